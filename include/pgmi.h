@@ -1,0 +1,143 @@
+/*
+ * pgmi.h -- C ABI of libpgmi, the MI355X-native (gfx950) PaliGemma-3B inference path.
+ *
+ * This is the drop-in boundary below the reference's Python API
+ * (PaliGemmaForConditionalGeneration / SiglipVisionModel / GemmaForCausalLM / KVCache in
+ * /root/reference/modeling_gemma.py and modeling_siglip.py).  The reference itself has no
+ * FFI -- it is pure PyTorch -- so each entry point names the reference function whose body it
+ * replaces; INTEGRATION.md shows the ctypes binding a maintainer would add.
+ *
+ * Conventions
+ *   - plain C, every call returns 0 on success or a negative PGMI_E* code; the message of the
+ *     last failure on the calling thread is pgmi_last_error().
+ *   - device pointers are HIP device memory of the context's device; streams are hipStream_t
+ *     passed as void* (NULL = the default stream).  Calls are stream-ordered and do not
+ *     synchronise unless stated.
+ *   - bf16 tensors are raw uint16 bit patterns, row-major, contiguous.
+ *   - one context per GPU; a context is not re-entrant (the reference is single-threaded).
+ */
+#ifndef PGMI_H
+#define PGMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGMI_OK 0
+#define PGMI_E_ARG -1     /* ValueError in the Python layer   */
+#define PGMI_E_STATE -2   /* AssertionError / misuse          */
+#define PGMI_E_HIP -3     /* HIP runtime error                */
+#define PGMI_E_NOMEM -4   /* allocation failure               */
+
+#define PGMI_DTYPE_BF16 0
+#define PGMI_DTYPE_F16 1
+#define PGMI_DTYPE_F32 2
+
+typedef struct pgmi_ctx pgmi_ctx;
+
+/* Mirrors SiglipVisionConfig (modeling_siglip.py:7-34), GemmaConfig (modeling_gemma.py:39-71)
+ * and PaliGemmaConfig (modeling_gemma.py:74-105), plus workspace capacities. */
+typedef struct pgmi_config {
+    int v_hidden, v_intermediate, v_layers, v_heads, v_channels, v_image, v_patch;
+    float v_ln_eps;
+    int t_vocab, t_hidden, t_intermediate, t_layers, t_heads, t_kv_heads, t_head_dim, t_max_pos;
+    float t_rms_eps, t_rope_theta;
+    int projection_dim;
+    int64_t image_token_index;
+    int64_t pad_token_id; /* -1 when the config's pad_token_id is None (modeling_gemma.py:453) */
+    int max_batch;        /* sequences / images per call                                    */
+    int max_seq;          /* longest prefill (image + text tokens)                          */
+    int max_kv;           /* KV-cache capacity in tokens (decode attention scratch)          */
+} pgmi_config;
+
+const char* pgmi_last_error(void);
+const char* pgmi_version(void);
+
+/* PaliGemmaForConditionalGeneration.__init__ (modeling_gemma.py:442-453): builds the weight
+ * layout; device memory is touched only by the calls below. */
+int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out);
+int pgmi_destroy(pgmi_ctx* ctx);
+
+/* ---- weights: one bf16 slab in caller-owned device memory, laid out by the library.
+ * Tensor names and shapes are the reference state-dict keys; lm_head is
+ * tied to embed_tokens (modeling_gemma.py:396-397) and has no slot of its own. */
+int64_t pgmi_weights_bytes(const pgmi_ctx* ctx);
+int pgmi_weight_count(const pgmi_ctx* ctx);
+int pgmi_weight_info(const pgmi_ctx* ctx, int idx, const char** name, int64_t* offset_bytes, int64_t* shape4,
+                     int* ndim);
+int pgmi_bind_weights(pgmi_ctx* ctx, void* dev_slab);
+/* load_state_dict for one tensor (utils.py:30-38 / ablation_study_fixed.py:315-320): copies
+ * (and converts to bf16) from host or device memory into the slab. */
+int pgmi_load_weight(pgmi_ctx* ctx, const char* name, const void* src, int src_dtype, int src_on_device,
+                     void* stream);
+/* deterministic synthetic weights (benchmarks; oracle/wgen.c recipe) */
+int pgmi_fill_synthetic(pgmi_ctx* ctx, const char* name, uint64_t key, float scale, float offset, void* stream);
+uint64_t pgmi_synthetic_key(const char* name, uint64_t seed);
+/* GemmaRotaryEmbedding.inv_freq (modeling_gemma.py:151), host fp32[head_dim/2]; default is
+ * 1/theta^(2i/d) computed as the reference does. */
+int pgmi_set_rope_inv_freq(pgmi_ctx* ctx, const float* inv_freq);
+/* optional exact cos/sin table (bf16 [max_pos][head_dim/2]) as torch computes it (:178-185) */
+int pgmi_set_rope_table(pgmi_ctx* ctx, const uint16_t* cos_tab, const uint16_t* sin_tab, int max_pos);
+/* derived device tensors (padded patch-embedding matrix, RoPE table, workspace). Call after
+ * the weights are in the slab and before the first forward; synchronises the device. */
+int pgmi_prepare(pgmi_ctx* ctx);
+
+/* ---- KV cache (KVCache, modeling_gemma.py:10-36): caller-owned slab
+ * [layer][K|V][batch][max_tokens][kv_heads*head_dim] bf16 */
+int64_t pgmi_kv_bytes(const pgmi_ctx* ctx, int batch, int max_tokens);
+
+/* ---- forward pieces -------------------------------------------------------------------- */
+/* SiglipVisionModel.forward (modeling_siglip.py:236-255) incl. the pixel cast of
+ * modeling_gemma.py:570: pixels (B,C,H,W) fp32 or bf16 -> feats (B, N, v_hidden) bf16 */
+int pgmi_vision(pgmi_ctx* ctx, const void* pixels, int pixel_dtype, int B, void* feats, void* stream);
+/* PaliGemmaMultiModalProjector.forward (modeling_gemma.py:435-438): (rows, v_hidden) -> (rows, proj) */
+int pgmi_project(pgmi_ctx* ctx, const void* feats, int rows, void* out, void* stream);
+/* nn.Embedding lookup of GemmaModel.embed_tokens (modeling_gemma.py:565) */
+int pgmi_embed(pgmi_ctx* ctx, const int64_t* ids, int rows, void* out, void* stream);
+/* GemmaForCausalLM.forward (modeling_gemma.py:399-427) over the merged embeddings of
+ * _merge_input_ids_with_image_features (modeling_gemma.py:468-537):
+ *   ids (device int64 B x L) and image_feats (projected, n_img_rows x hidden, may be NULL) are
+ *   merged on the device; if embeds != NULL they are used instead (already-merged embeddings,
+ *   e.g. from a monkey-patched merge) and ids/image_feats are ignored.
+ *   positions: HOST int64 B x L (rotary positions, modeling_gemma.py:516-535).
+ *   KV: keys/values of the L tokens are written at rows kv_start.. of the caller's slab;
+ *   attention covers rows [0, kv_start + L) (the reference's zero mask: non-causal).
+ *   logits (device fp32): logits_rows == 0 -> (B, L, vocab); 1 -> (B, 1, vocab) last row only. */
+int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, int n_img_rows, const void* embeds,
+                    int B, int L, const int64_t* positions, void* kv, int kv_batch, int kv_max, int kv_start,
+                    float* logits, int logits_rows, void* stream);
+/* One KV-cached decode step for B sequences in lock-step (inference.py:56-78 loop body):
+ *   ids (device int64 [B]), written at KV row kv_len, rotary position `position`
+ *   (= attention_mask.cumsum(-1)[:, -1], modeling_gemma.py:526, i.e. kv_len + 1 after an
+ *   inference.py prefill), attention over rows [0, kv_len]; logits (device fp32 [B][vocab]);
+ *   next_ids (device int64 [B], may be NULL) = argmax (first max, torch.argmax semantics).
+ *   use_graph != 0 replays a captured hipGraph of the whole step. */
+int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
+/* torch.argmax(logits, -1) over rows of a device fp32 [rows][V] matrix (inference.py:68) */
+int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* out, void* stream);
+
+/* ---- single-op entry points (kernel-level parity tests) ---------------------------------- */
+/* out = epilogue(A[M,K] . W[N,K]^T): epi 0 store, 1 +bias, 2 +bias,gelu, 3 +bias,+res, 4 +res,
+ * 6 fp32 out (out is float*), 7 GeGLU with up rows at W + N*K */
+int pgmi_op_gemm(pgmi_ctx* ctx, const void* A, const void* W, int M, int N, int K, int epi, const void* bias,
+                 const void* res, void* out, void* stream);
+int pgmi_op_rmsnorm(pgmi_ctx* ctx, const void* x, const void* w, int rows, int D, float eps, void* out,
+                    void* stream);
+int pgmi_op_layernorm(pgmi_ctx* ctx, const void* x, const void* w, const void* b, int rows, int D, float eps,
+                      void* out, void* stream);
+/* attention over q (B, Lq, H, hd), k/v (B, Lk, Hkv, hd) -> o (B, Lq, H, hd), all contiguous bf16;
+ * s = bf16(bf16(q.k) * scale) */
+int pgmi_op_attention(pgmi_ctx* ctx, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk,
+                      int H, int Hkv, int head_dim, float scale, void* stream);
+/* decode GEMV family on one layer's weights (tests): y[b][n] += W x (residual form) */
+int pgmi_op_gemv_res(pgmi_ctx* ctx, const void* x, const void* W, int B, int N, int K, void* h_inout,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGMI_H */

@@ -1,0 +1,75 @@
+// common.h -- shared device helpers for libpgmi (gfx950 / CDNA4 only).
+//
+// bf16 is carried as raw uint16 bit patterns; all arithmetic is fp32 with an
+// explicit round-to-nearest-even back to bf16 exactly where the reference's bf16
+// PyTorch modules round ("rounding points").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pgmi {
+
+typedef uint16_t bf16_t;
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+struct alignas(16) u16x8 { uint16_t v[8]; };
+
+__device__ __forceinline__ float bf2f(uint16_t b) {
+    return __uint_as_float(((uint32_t)b) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (inputs here are finite; a NaN stays NaN-ish)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+
+// gelu(approximate="tanh") in fp32 (torch: 0.5*x*(1+tanh(sqrt(2/pi)*(x+0.044715*x^3))))
+__device__ __forceinline__ float gelu_tanh(float x) {
+    const float k = 0.7978845608028654f;
+    float inner = k * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(inner));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// 8 bf16 (16 B) dot 8 bf16 with fp32 accumulation via v_dot2_f32_bf16
+__device__ __forceinline__ float dot8(const uint4 a, const uint4 b, float acc) {
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a.x), __builtin_bit_cast(bf16x2, b.x), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a.y), __builtin_bit_cast(bf16x2, b.y), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a.z), __builtin_bit_cast(bf16x2, b.z), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a.w), __builtin_bit_cast(bf16x2, b.w), acc, false);
+    return acc;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ldg_nt(const void* p) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint4 ldg16(const void* p) {
+    return *reinterpret_cast<const uint4*>(p);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const short8 a, const short8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace pgmi

@@ -1,0 +1,736 @@
+// engine.hip -- libpgmi host side: weight layout, workspaces, forward orchestration, hipGraph
+// decode, and the extern "C" ABI declared in include/pgmi.h.
+//
+// Orchestration restates the reference's call stacks:
+//   vision   SiglipVisionTransformer.forward   modeling_siglip.py:236-244
+//   lm       GemmaModel/GemmaForCausalLM        modeling_gemma.py:357-427
+//   decode   one inference.py loop iteration    inference.py:56-78
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pgmi.h"
+#include "common.h"
+#include "launch.h"
+
+using namespace pgmi;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail(PGMI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LAUNCHCHK()                                                                        \
+    do {                                                                                   \
+        hipError_t e_ = hipGetLastError();                                                 \
+        if (e_ != hipSuccess) return fail(PGMI_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Slot {
+    std::string name;
+    int64_t off;
+    int64_t shape[4];
+    int ndim;
+    int64_t numel;
+};
+
+struct GraphKey {
+    int B;
+    void* kv;
+    int kv_batch, kv_max;
+    float* logits;
+    int64_t* next;
+    bool operator<(const GraphKey& o) const {
+        return std::tie(B, kv, kv_batch, kv_max, logits, next) < std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next);
+    }
+};
+
+struct GraphEntry {
+    int seen = 0;
+    hipGraphExec_t exec = nullptr;
+};
+
+struct pgmi_ctx {
+    pgmi_config c;
+    int device;
+    std::vector<Slot> slots;
+    std::unordered_map<std::string, int> index;
+    int64_t slab_bytes = 0;
+    uint8_t* slab = nullptr;
+    std::vector<float> inv_freq;
+    std::vector<uint16_t> host_cos, host_sin;  // optional exact table
+    bool prepared = false;
+    std::vector<void*> allocs;
+    // derived
+    uint16_t* patch_w = nullptr;  // [v_hidden][kpad]
+    int kpad = 0;
+    uint16_t* cosT = nullptr;
+    uint16_t* sinT = nullptr;
+    // text prefill workspace (rows = max_batch*max_seq)
+    uint16_t *Hs, *Tn, *QKV, *Qr, *AO, *ACT, *lastrows;
+    int64_t* dpos;
+    int64_t* dids_tmp;
+    // vision workspace (rows = max_batch*N)
+    uint16_t *vX, *vT, *vQKV, *vAO, *vH, *vP;
+    float* ws;
+    size_t ws_bytes;
+    // decode workspace
+    uint16_t *dH, *dQ, *dAO, *dACT;
+    float *scores, *opart, *pmax;
+    int* pidx;
+    int max_chunks;
+    StepState* step;
+    int64_t* d_ids;
+    hipStream_t cap_stream = nullptr;
+    std::map<GraphKey, GraphEntry> graphs;
+};
+
+namespace {
+
+int n_img(const pgmi_config& c) { return (c.v_image / c.v_patch) * (c.v_image / c.v_patch); }
+
+void add_slot(pgmi_ctx* x, const std::string& name, std::initializer_list<int64_t> shape) {
+    Slot s;
+    s.name = name;
+    s.ndim = (int)shape.size();
+    s.numel = 1;
+    int i = 0;
+    for (int64_t d : shape) { s.shape[i++] = d; s.numel *= d; }
+    for (; i < 4; ++i) s.shape[i] = 1;
+    s.off = x->slab_bytes;
+    x->slab_bytes += (s.numel * 2 + 255) / 256 * 256;
+    x->index[name] = (int)x->slots.size();
+    x->slots.push_back(s);
+}
+
+// Slab layout: the reference state-dict tensors, ordered so that the projections that are
+// fused into one GEMM/GEMV are adjacent (q|k|v weights and biases, gate|up).
+void build_layout(pgmi_ctx* x) {
+    const pgmi_config& c = x->c;
+    const int64_t D = c.v_hidden, I = c.v_intermediate, P = c.v_patch, C = c.v_channels, N = n_img(c);
+    const std::string vp = "vision_tower.vision_model.";
+    add_slot(x, vp + "embeddings.patch_embedding.weight", {D, C, P, P});
+    add_slot(x, vp + "embeddings.patch_embedding.bias", {D});
+    add_slot(x, vp + "embeddings.position_embedding.weight", {N, D});
+    for (int i = 0; i < c.v_layers; ++i) {
+        const std::string lp = vp + "encoder.layers." + std::to_string(i) + ".";
+        for (const char* nm : {"q_proj", "k_proj", "v_proj"}) add_slot(x, lp + "self_attn." + nm + ".weight", {D, D});
+        for (const char* nm : {"q_proj", "k_proj", "v_proj"}) add_slot(x, lp + "self_attn." + nm + ".bias", {D});
+        add_slot(x, lp + "self_attn.out_proj.weight", {D, D});
+        add_slot(x, lp + "self_attn.out_proj.bias", {D});
+        add_slot(x, lp + "layer_norm1.weight", {D});
+        add_slot(x, lp + "layer_norm1.bias", {D});
+        add_slot(x, lp + "mlp.fc1.weight", {I, D});
+        add_slot(x, lp + "mlp.fc1.bias", {I});
+        add_slot(x, lp + "mlp.fc2.weight", {D, I});
+        add_slot(x, lp + "mlp.fc2.bias", {D});
+        add_slot(x, lp + "layer_norm2.weight", {D});
+        add_slot(x, lp + "layer_norm2.bias", {D});
+    }
+    add_slot(x, vp + "post_layernorm.weight", {D});
+    add_slot(x, vp + "post_layernorm.bias", {D});
+    add_slot(x, "multi_modal_projector.linear.weight", {c.projection_dim, D});
+    add_slot(x, "multi_modal_projector.linear.bias", {c.projection_dim});
+    const int64_t H = c.t_hidden, TI = c.t_intermediate, V = c.t_vocab, HD = c.t_head_dim;
+    add_slot(x, "language_model.model.embed_tokens.weight", {V, H});
+    for (int i = 0; i < c.t_layers; ++i) {
+        const std::string lp = "language_model.model.layers." + std::to_string(i) + ".";
+        add_slot(x, lp + "self_attn.q_proj.weight", {c.t_heads * HD, H});
+        add_slot(x, lp + "self_attn.k_proj.weight", {c.t_kv_heads * HD, H});
+        add_slot(x, lp + "self_attn.v_proj.weight", {c.t_kv_heads * HD, H});
+        add_slot(x, lp + "self_attn.o_proj.weight", {H, c.t_heads * HD});
+        add_slot(x, lp + "mlp.gate_proj.weight", {TI, H});
+        add_slot(x, lp + "mlp.up_proj.weight", {TI, H});
+        add_slot(x, lp + "mlp.down_proj.weight", {H, TI});
+        add_slot(x, lp + "input_layernorm.weight", {H});
+        add_slot(x, lp + "post_attention_layernorm.weight", {H});
+    }
+    add_slot(x, "language_model.model.norm.weight", {H});
+}
+
+inline uint16_t* W(pgmi_ctx* x, const std::string& name) {
+    auto it = x->index.find(name);
+    if (it == x->index.end()) return nullptr;
+    return reinterpret_cast<uint16_t*>(x->slab + x->slots[it->second].off);
+}
+
+inline uint16_t* VL(pgmi_ctx* x, int i, const char* suffix) {
+    return W(x, "vision_tower.vision_model.encoder.layers." + std::to_string(i) + "." + suffix);
+}
+inline uint16_t* TL(pgmi_ctx* x, int i, const char* suffix) {
+    return W(x, "language_model.model.layers." + std::to_string(i) + "." + suffix);
+}
+
+uint16_t host_f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+float bf16_round_host(float f) {
+    uint32_t u = (uint32_t)host_f2bf(f) << 16;
+    float r;
+    std::memcpy(&r, &u, 4);
+    return r;
+}
+
+uint64_t fnv1a(const char* s) {
+    uint64_t h = 0xCBF29CE484222325ULL;
+    for (const unsigned char* p = (const unsigned char*)s; *p; ++p) { h ^= *p; h *= 0x100000001B3ULL; }
+    return h;
+}
+
+uint64_t splitmix64_h(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__global__ void k_convert(const void* src, int dtype, long n, uint16_t* dst) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        if (dtype == PGMI_DTYPE_F32) dst[i] = f2bf(reinterpret_cast<const float*>(src)[i]);
+        else dst[i] = f2bf((float)reinterpret_cast<const _Float16*>(src)[i]);
+    }
+}
+
+int dalloc(pgmi_ctx* x, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 256;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(PGMI_E_NOMEM, std::string("hipMalloc ") + std::to_string(bytes) + ": " + hipGetErrorString(e));
+    x->allocs.push_back(*p);
+    return 0;
+}
+
+template <typename T>
+int dalloc_t(pgmi_ctx* x, T** p, size_t count) {
+    return dalloc(x, reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+// RoPE tables: freqs = fp32(pos * inv_freq) (modeling_gemma.py:178), cos/sin in fp32 (:182-183),
+// cast to bf16 (:185).  cos/sin of the fp32 angle are evaluated in double and rounded once.
+void build_rope_host(pgmi_ctx* x, std::vector<uint16_t>& cs, std::vector<uint16_t>& sn) {
+    const int half = x->c.t_head_dim / 2, mp = x->c.t_max_pos;
+    cs.resize((size_t)mp * half);
+    sn.resize((size_t)mp * half);
+    for (int p = 0; p < mp; ++p)
+        for (int i = 0; i < half; ++i) {
+            const float ang = (float)p * x->inv_freq[i];
+            cs[(size_t)p * half + i] = host_f2bf((float)std::cos((double)ang));
+            sn[(size_t)p * half + i] = host_f2bf((float)std::sin((double)ang));
+        }
+}
+
+int ensure_prepared(pgmi_ctx* x) {
+    if (!x->prepared) return fail(PGMI_E_STATE, "pgmi_prepare() has not been called");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound (pgmi_bind_weights)");
+    return 0;
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+extern "C" {
+
+const char* pgmi_last_error(void) { return g_err.c_str(); }
+const char* pgmi_version(void) { return "pgmi 0.1.0 (gfx950)"; }
+
+int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
+    if (!cfg || !out) return fail(PGMI_E_ARG, "null argument");
+    const pgmi_config& c = *cfg;
+    if (c.t_head_dim != 256) return fail(PGMI_E_ARG, "head_dim must be 256 (Gemma)");
+    if (c.t_hidden != 2048) return fail(PGMI_E_ARG, "text hidden must be 2048 (decode kernels are specialised)");
+    if (c.t_intermediate % 8 != 0 || c.v_intermediate % 8 != 0) return fail(PGMI_E_ARG, "intermediate sizes must be multiples of 8");
+    if (c.v_hidden % c.v_heads != 0 || c.v_hidden / c.v_heads != 72) return fail(PGMI_E_ARG, "SigLIP head_dim must be 72");
+    if (c.t_heads % c.t_kv_heads != 0 || c.t_heads / c.t_kv_heads > 16) return fail(PGMI_E_ARG, "at most 16 query heads per kv head");
+    if (c.max_batch < 1 || c.max_batch > 8) return fail(PGMI_E_ARG, "max_batch must be in [1, 8]");
+    if (c.v_hidden > 4096) return fail(PGMI_E_ARG, "v_hidden too large for the LayerNorm kernel");
+    auto* x = new pgmi_ctx();
+    x->c = c;
+    if (x->c.max_kv <= 0) x->c.max_kv = c.t_max_pos;
+    x->device = device;
+    build_layout(x);
+    x->inv_freq.resize(c.t_head_dim / 2);
+    for (int i = 0; i < c.t_head_dim / 2; ++i) {
+        // 1.0 / (base ** (arange(0, dim, 2).float() / dim)), fp32 (modeling_gemma.py:151)
+        const float e = (float)(2 * i) / (float)c.t_head_dim;
+        const float p = (float)std::pow((double)c.t_rope_theta, (double)e);
+        x->inv_freq[i] = 1.0f / p;
+    }
+    *out = x;
+    return 0;
+}
+
+int pgmi_destroy(pgmi_ctx* x) {
+    if (!x) return 0;
+    for (auto& kv : x->graphs)
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    for (void* p : x->allocs) (void)hipFree(p);
+    if (x->cap_stream) (void)hipStreamDestroy(x->cap_stream);
+    delete x;
+    return 0;
+}
+
+int64_t pgmi_weights_bytes(const pgmi_ctx* x) { return x ? x->slab_bytes : -1; }
+int pgmi_weight_count(const pgmi_ctx* x) { return x ? (int)x->slots.size() : -1; }
+
+int pgmi_weight_info(const pgmi_ctx* x, int idx, const char** name, int64_t* off, int64_t* shape4, int* ndim) {
+    if (!x || idx < 0 || idx >= (int)x->slots.size()) return fail(PGMI_E_ARG, "weight index out of range");
+    const Slot& s = x->slots[idx];
+    if (name) *name = s.name.c_str();
+    if (off) *off = s.off;
+    if (shape4) for (int i = 0; i < 4; ++i) shape4[i] = s.shape[i];
+    if (ndim) *ndim = s.ndim;
+    return 0;
+}
+
+int pgmi_bind_weights(pgmi_ctx* x, void* slab) {
+    if (!x || !slab) return fail(PGMI_E_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(slab) % 256 != 0) return fail(PGMI_E_ARG, "weight slab must be 256-byte aligned");
+    x->slab = reinterpret_cast<uint8_t*>(slab);
+    x->graphs.clear();
+    return 0;
+}
+
+int pgmi_load_weight(pgmi_ctx* x, const char* name, const void* src, int dtype, int on_device, void* stream) {
+    if (!x || !name || !src) return fail(PGMI_E_ARG, "null argument");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound");
+    auto it = x->index.find(name);
+    if (it == x->index.end()) return fail(PGMI_E_ARG, std::string("unknown weight ") + name);
+    const Slot& s = x->slots[it->second];
+    uint16_t* dst = reinterpret_cast<uint16_t*>(x->slab + s.off);
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(x->device));
+    if (dtype == PGMI_DTYPE_BF16) {
+        HIPCHK(hipMemcpyAsync(dst, src, s.numel * 2, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    } else if (dtype == PGMI_DTYPE_F32 || dtype == PGMI_DTYPE_F16) {
+        if (on_device) {
+            hipLaunchKernelGGL(k_convert, dim3(1024), dim3(256), 0, st, src, dtype, (long)s.numel, dst);
+            LAUNCHCHK();
+        } else {
+            std::vector<uint16_t> tmp(s.numel);
+            for (int64_t i = 0; i < s.numel; ++i) {
+                float f = dtype == PGMI_DTYPE_F32 ? reinterpret_cast<const float*>(src)[i]
+                                                 : (float)reinterpret_cast<const _Float16*>(src)[i];
+                tmp[i] = host_f2bf(f);
+            }
+            HIPCHK(hipMemcpyAsync(dst, tmp.data(), s.numel * 2, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+    } else {
+        return fail(PGMI_E_ARG, "unsupported dtype");
+    }
+    return 0;
+}
+
+uint64_t pgmi_synthetic_key(const char* name, uint64_t seed) { return splitmix64_h(seed ^ fnv1a(name)); }
+
+int pgmi_fill_synthetic(pgmi_ctx* x, const char* name, uint64_t key, float scale, float offset, void* stream) {
+    if (!x || !name) return fail(PGMI_E_ARG, "null argument");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound");
+    auto it = x->index.find(name);
+    if (it == x->index.end()) return fail(PGMI_E_ARG, std::string("unknown weight ") + name);
+    const Slot& s = x->slots[it->second];
+    HIPCHK(hipSetDevice(x->device));
+    fill_synthetic((hipStream_t)stream, reinterpret_cast<uint16_t*>(x->slab + s.off), (long)s.numel, key, scale, offset);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_set_rope_inv_freq(pgmi_ctx* x, const float* inv) {
+    if (!x || !inv) return fail(PGMI_E_ARG, "null argument");
+    for (int i = 0; i < x->c.t_head_dim / 2; ++i) x->inv_freq[i] = inv[i];
+    x->host_cos.clear();
+    x->host_sin.clear();
+    x->prepared = false;
+    return 0;
+}
+
+int pgmi_set_rope_table(pgmi_ctx* x, const uint16_t* cs, const uint16_t* sn, int max_pos) {
+    if (!x || !cs || !sn) return fail(PGMI_E_ARG, "null argument");
+    if (max_pos != x->c.t_max_pos) return fail(PGMI_E_ARG, "rope table must cover max_position_embeddings");
+    const size_t n = (size_t)max_pos * (x->c.t_head_dim / 2);
+    x->host_cos.assign(cs, cs + n);
+    x->host_sin.assign(sn, sn + n);
+    x->prepared = false;
+    return 0;
+}
+
+int pgmi_prepare(pgmi_ctx* x) {
+    if (!x) return fail(PGMI_E_ARG, "null argument");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound");
+    HIPCHK(hipSetDevice(x->device));
+    const pgmi_config& c = x->c;
+    int rc;
+    if (!x->cosT) {
+        const int N = n_img(c);
+        const size_t R = (size_t)c.max_batch * c.max_seq, RV = (size_t)c.max_batch * N;
+        const int H = c.t_hidden, QKVN = (c.t_heads + 2 * c.t_kv_heads) * c.t_head_dim;
+        x->kpad = (c.v_channels * c.v_patch * c.v_patch + 63) / 64 * 64;
+        if ((rc = dalloc_t(x, &x->patch_w, (size_t)c.v_hidden * x->kpad))) return rc;
+        if ((rc = dalloc_t(x, &x->cosT, (size_t)c.t_max_pos * c.t_head_dim / 2))) return rc;
+        if ((rc = dalloc_t(x, &x->sinT, (size_t)c.t_max_pos * c.t_head_dim / 2))) return rc;
+        if ((rc = dalloc_t(x, &x->Hs, R * H))) return rc;
+        if ((rc = dalloc_t(x, &x->Tn, R * H))) return rc;
+        if ((rc = dalloc_t(x, &x->QKV, R * QKVN))) return rc;
+        if ((rc = dalloc_t(x, &x->Qr, R * c.t_heads * c.t_head_dim))) return rc;
+        if ((rc = dalloc_t(x, &x->AO, R * H))) return rc;
+        if ((rc = dalloc_t(x, &x->ACT, R * c.t_intermediate))) return rc;
+        if ((rc = dalloc_t(x, &x->lastrows, (size_t)c.max_batch * H))) return rc;
+        if ((rc = dalloc_t(x, &x->dpos, R))) return rc;
+        if ((rc = dalloc_t(x, &x->dids_tmp, R))) return rc;
+        if ((rc = dalloc_t(x, &x->vX, RV * c.v_hidden))) return rc;
+        if ((rc = dalloc_t(x, &x->vT, RV * c.v_hidden))) return rc;
+        if ((rc = dalloc_t(x, &x->vQKV, RV * 3 * c.v_hidden))) return rc;
+        if ((rc = dalloc_t(x, &x->vAO, RV * c.v_hidden))) return rc;
+        if ((rc = dalloc_t(x, &x->vH, RV * c.v_intermediate))) return rc;
+        if ((rc = dalloc_t(x, &x->vP, RV * x->kpad))) return rc;
+        x->ws_bytes = (size_t)64 << 20;
+        if ((rc = dalloc(x, reinterpret_cast<void**>(&x->ws), x->ws_bytes))) return rc;
+        const int B = c.max_batch;
+        if ((rc = dalloc_t(x, &x->dH, (size_t)B * H))) return rc;
+        if ((rc = dalloc_t(x, &x->dQ, (size_t)B * c.t_heads * c.t_head_dim))) return rc;
+        if ((rc = dalloc_t(x, &x->dAO, (size_t)B * H))) return rc;
+        if ((rc = dalloc_t(x, &x->dACT, (size_t)B * c.t_intermediate))) return rc;
+        x->max_chunks = (c.max_kv + 63) / 64;
+        if ((rc = dalloc_t(x, &x->scores, (size_t)B * c.t_kv_heads * 16 * c.max_kv))) return rc;
+        if ((rc = dalloc_t(x, &x->opart, (size_t)B * c.t_kv_heads * x->max_chunks * 16 * 256))) return rc;
+        if ((rc = dalloc_t(x, &x->pmax, (size_t)B * gemv_logits_blocks()))) return rc;
+        if ((rc = dalloc_t(x, &x->pidx, (size_t)B * gemv_logits_blocks()))) return rc;
+        if ((rc = dalloc_t(x, &x->step, 1))) return rc;
+        if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
+        HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
+    }
+    // derived tensors
+    pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
+             c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
+    LAUNCHCHK();
+    std::vector<uint16_t> cs, sn;
+    if (!x->host_cos.empty()) {
+        cs = x->host_cos;
+        sn = x->host_sin;
+    } else {
+        build_rope_host(x, cs, sn);
+    }
+    HIPCHK(hipMemcpy(x->cosT, cs.data(), cs.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(x->sinT, sn.data(), sn.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipDeviceSynchronize());
+    for (auto& kv : x->graphs)
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    x->graphs.clear();
+    x->prepared = true;
+    return 0;
+}
+
+int64_t pgmi_kv_bytes(const pgmi_ctx* x, int batch, int max_tokens) {
+    if (!x) return -1;
+    return (int64_t)x->c.t_layers * 2 * batch * max_tokens * x->c.t_kv_heads * x->c.t_head_dim * 2;
+}
+
+int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    const pgmi_config& c = x->c;
+    if (B < 1 || B > c.max_batch) return fail(PGMI_E_ARG, "batch exceeds max_batch");
+    if (!pixels || !feats) return fail(PGMI_E_ARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const int N = n_img(c), D = c.v_hidden, Iv = c.v_intermediate, rows = B * N;
+    const float eps = c.v_ln_eps;
+    patchify(s, pixels, dtype == PGMI_DTYPE_F32, B, c.v_channels, c.v_image, c.v_image, c.v_patch, x->kpad, x->vP);
+    // Conv2d + bias + position embedding (modeling_siglip.py:67,76)
+    EpiArgs e{};
+    e.bias = W(x, "vision_tower.vision_model.embeddings.patch_embedding.bias");
+    e.pos = W(x, "vision_tower.vision_model.embeddings.position_embedding.weight");
+    e.npos = N;
+    e.out = x->vX;
+    e.ldo = D;
+    gemm(s, x->vP, x->kpad, x->patch_w, x->kpad, rows, D, x->kpad, EPI_BIAS_POS, e, x->ws, x->ws_bytes);
+    const float scale = (float)std::pow((double)(D / c.v_heads), -0.5);  // head_dim**-0.5 (:89)
+    for (int i = 0; i < c.v_layers; ++i) {
+        layernorm(s, x->vX, VL(x, i, "layer_norm1.weight"), VL(x, i, "layer_norm1.bias"), eps, x->vT, rows, D);
+        EpiArgs q{};
+        q.bias = VL(x, i, "self_attn.q_proj.bias");  // q|k|v biases adjacent
+        q.out = x->vQKV;
+        q.ldo = 3 * D;
+        gemm(s, x->vT, D, VL(x, i, "self_attn.q_proj.weight"), D, rows, 3 * D, D, EPI_BIAS, q, x->ws, x->ws_bytes);
+        AttnArgs a{};
+        a.q = x->vQKV; a.q_b_stride = (long)N * 3 * D; a.q_row_stride = 3 * D; a.q_head_stride = 72;
+        a.k = x->vQKV + D; a.k_b_stride = a.q_b_stride; a.k_row_stride = 3 * D; a.k_head_stride = 72;
+        a.v = x->vQKV + 2 * D; a.v_b_stride = a.q_b_stride; a.v_row_stride = 3 * D; a.v_head_stride = 72;
+        a.o = x->vAO; a.o_b_stride = (long)N * D; a.o_row_stride = D; a.o_head_stride = 72;
+        a.Lq = N; a.Lk = N; a.G = 1; a.n_kv = c.v_heads; a.B = B; a.scale = scale;
+        attention_prefill(s, 72, a);
+        EpiArgs o{};
+        o.bias = VL(x, i, "self_attn.out_proj.bias");
+        o.res = x->vX; o.ldr = D; o.out = x->vX; o.ldo = D;
+        gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws, x->ws_bytes);
+        layernorm(s, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"), eps, x->vT, rows, D);
+        EpiArgs f1{};
+        f1.bias = VL(x, i, "mlp.fc1.bias"); f1.out = x->vH; f1.ldo = Iv;
+        gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
+        EpiArgs f2{};
+        f2.bias = VL(x, i, "mlp.fc2.bias"); f2.res = x->vX; f2.ldr = D; f2.out = x->vX; f2.ldo = D;
+        gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws, x->ws_bytes);
+    }
+    layernorm(s, x->vX, W(x, "vision_tower.vision_model.post_layernorm.weight"),
+              W(x, "vision_tower.vision_model.post_layernorm.bias"), eps, reinterpret_cast<uint16_t*>(feats), rows, D);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_project(pgmi_ctx* x, const void* feats, int rows, void* out, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (!feats || !out || rows < 1) return fail(PGMI_E_ARG, "bad argument");
+    if (rows > x->c.max_batch * n_img(x->c)) return fail(PGMI_E_ARG, "rows exceed workspace capacity");
+    EpiArgs e{};
+    e.bias = W(x, "multi_modal_projector.linear.bias");
+    e.out = reinterpret_cast<uint16_t*>(out);
+    e.ldo = x->c.projection_dim;
+    gemm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(feats), x->c.v_hidden,
+         W(x, "multi_modal_projector.linear.weight"), x->c.v_hidden, rows, x->c.projection_dim, x->c.v_hidden,
+         EPI_BIAS, e, x->ws, x->ws_bytes);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_embed(pgmi_ctx* x, const int64_t* ids, int rows, void* out, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (!ids || !out) return fail(PGMI_E_ARG, "null argument");
+    // plain lookup: normalizer 1, no pad zeroing (nn.Embedding, modeling_gemma.py:565)
+    embed_rows((hipStream_t)stream, ids, rows, W(x, "language_model.model.embed_tokens.weight"), x->c.t_hidden,
+               1.0f, INT64_MIN, reinterpret_cast<uint16_t*>(out));
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, int n_img_rows, const void* embeds,
+                    int B, int L, const int64_t* positions, void* kv, int kv_batch, int kv_max, int kv_start,
+                    float* logits, int logits_rows, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    const pgmi_config& c = x->c;
+    if (B < 1 || B > c.max_batch || B > kv_batch) return fail(PGMI_E_ARG, "batch exceeds capacity");
+    if (L < 1 || L > c.max_seq) return fail(PGMI_E_ARG, "sequence length exceeds max_seq");
+    if (kv_start < 0 || kv_start + L > kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
+    if (kv_start + L > attention_prefill_max_keys(256)) return fail(PGMI_E_ARG, "prefill attention span too long");
+    if (!positions || !kv || !logits || (!embeds && !ids)) return fail(PGMI_E_ARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const int H = c.t_hidden, R = B * L, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
+    const int QKVN = (NH + 2 * NKV) * HD;
+    const float eps = c.t_rms_eps;
+    const float normalizer = bf16_round_host(std::sqrt((float)H));  // torch.tensor(H**0.5, dtype=bf16) (:367)
+    const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
+    HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)R * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (embeds) {
+        scale_rows(s, reinterpret_cast<const uint16_t*>(embeds), (long)R * H, normalizer, x->Hs);
+    } else {
+        merge_embed(s, ids, B, L, E, H, reinterpret_cast<const uint16_t*>(image_feats), image_feats ? n_img_rows : 0,
+                    c.image_token_index, c.pad_token_id, (float)std::sqrt((double)H), normalizer, nullptr,
+                    reinterpret_cast<int*>(x->dids_tmp), x->Hs);
+    }
+    const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
+    uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
+    for (int i = 0; i < c.t_layers; ++i) {
+        uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
+        uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+        rmsnorm(s, x->Hs, TL(x, i, "input_layernorm.weight"), eps, x->Tn, R, H);
+        EpiArgs q{};
+        q.out = x->QKV; q.ldo = QKVN;
+        gemm(s, x->Tn, H, TL(x, i, "self_attn.q_proj.weight"), H, R, QKVN, H, EPI_STORE, q, x->ws, x->ws_bytes);
+        rope_kv_append(s, x->QKV, B, L, NH, NKV, x->dpos, x->cosT, x->sinT, c.t_max_pos, x->Qr, Kc, Vc, kvb, kv_start);
+        AttnArgs a{};
+        a.q = x->Qr; a.q_b_stride = (long)L * NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
+        a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
+        a.v = Vc; a.v_b_stride = kvb; a.v_row_stride = (int)kvd; a.v_head_stride = HD;
+        a.o = x->AO; a.o_b_stride = (long)L * H; a.o_row_stride = H; a.o_head_stride = HD;
+        a.Lq = L; a.Lk = kv_start + L; a.G = NH / NKV; a.n_kv = NKV; a.B = B;
+        a.scale = 1.0f / std::sqrt((float)HD);  // / math.sqrt(head_dim) (:266): exact power of two
+        attention_prefill(s, 256, a);
+        EpiArgs o{};
+        o.res = x->Hs; o.ldr = H; o.out = x->Hs; o.ldo = H;
+        gemm(s, x->AO, H, TL(x, i, "self_attn.o_proj.weight"), H, R, H, NH * HD, EPI_RES, o, x->ws, x->ws_bytes);
+        rmsnorm(s, x->Hs, TL(x, i, "post_attention_layernorm.weight"), eps, x->Tn, R, H);
+        EpiArgs g{};
+        g.out = x->ACT; g.ldo = c.t_intermediate;
+        gemm(s, x->Tn, H, TL(x, i, "mlp.gate_proj.weight"), H, R, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
+             x->ws_bytes, c.t_intermediate);
+        EpiArgs d{};
+        d.res = x->Hs; d.ldr = H; d.out = x->Hs; d.ldo = H;
+        gemm(s, x->ACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, R, H,
+             c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes);
+    }
+    const uint16_t* fnorm = W(x, "language_model.model.norm.weight");
+    if (logits_rows == 0) {
+        rmsnorm(s, x->Hs, fnorm, eps, x->Tn, R, H);
+        EpiArgs l{};
+        l.out_f32 = logits; l.ldo = c.t_vocab;
+        gemm(s, x->Tn, H, E, H, R, c.t_vocab, H, EPI_F32, l, x->ws, x->ws_bytes);
+    } else {
+        HIPCHK(hipMemcpy2DAsync(x->lastrows, (size_t)H * 2, x->Hs + (size_t)(L - 1) * H, (size_t)L * H * 2,
+                                (size_t)H * 2, B, hipMemcpyDeviceToDevice, s));
+        int nparts = 0;
+        gemv_logits(s, B, x->lastrows, fnorm, eps, E, c.t_vocab, logits, x->pmax, x->pidx, &nparts);
+    }
+    LAUNCHCHK();
+    return 0;
+}
+
+static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
+                       int launch_keys, float* logits, int64_t* next_ids) {
+    const pgmi_config& c = x->c;
+    const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
+    const float eps = c.t_rms_eps;
+    const float normalizer = bf16_round_host(std::sqrt((float)H));
+    const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
+    const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
+    uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
+    embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    for (int i = 0; i < c.t_layers; ++i) {
+        uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
+        uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+        gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
+                 x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb);
+        AttnArgs a{};
+        a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
+        a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
+        a.v = Vc; a.v_b_stride = kvb; a.v_row_stride = (int)kvd; a.v_head_stride = HD;
+        a.o = x->dAO; a.o_b_stride = (long)H; a.o_row_stride = H; a.o_head_stride = HD;
+        a.Lq = 1; a.Lk = 0; a.G = NH / NKV; a.n_kv = NKV; a.B = B; a.scale = 1.0f / std::sqrt((float)HD);
+        attention_decode(s, a, x->step, c.max_kv, launch_keys, x->scores, x->opart, x->max_chunks);
+        gemv_res(s, B, NH * HD, x->dAO, TL(x, i, "self_attn.o_proj.weight"), H, x->dH);
+        gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
+                   c.t_intermediate, x->dACT);
+        gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH);
+    }
+    int nparts = 0;
+    gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax, x->pidx,
+                &nparts);
+    if (next_ids) argmax_finish(s, B, x->pmax, x->pidx, nparts, next_ids);
+    return 0;
+}
+
+int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len, int position,
+                float* logits, int64_t* next_ids, int use_graph, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    const pgmi_config& c = x->c;
+    if (B < 1 || B > c.max_batch || B > kv_batch) return fail(PGMI_E_ARG, "batch exceeds capacity");
+    if (kv_len < 0 || kv_len >= kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
+    if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
+    if (!ids || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    set_step(s, x->step, kv_len, position);
+    if (!use_graph) {
+        decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids);
+        LAUNCHCHK();
+        return 0;
+    }
+    HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids};
+    GraphEntry& ge = x->graphs[key];
+    if (!ge.exec) {
+        if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
+            decode_body(x, s, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+            LAUNCHCHK();
+            return 0;
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        hipGraph_t g;
+        HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
+        decode_body(x, x->cap_stream, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+        HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
+        HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+    }
+    HIPCHK(hipGraphLaunch(ge.exec, s));
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_argmax(pgmi_ctx* x, const float* logits, int rows, int V, int64_t* out, void* stream) {
+    if (!x || !logits || !out) return fail(PGMI_E_ARG, "null argument");
+    argmax_rows((hipStream_t)stream, logits, rows, V, out);
+    LAUNCHCHK();
+    return 0;
+}
+
+// ---------------------------------------------------------------- single ops (tests)
+int pgmi_op_gemm(pgmi_ctx* x, const void* A, const void* Wt, int M, int N, int K, int epi, const void* bias,
+                 const void* res, void* out, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (K % 8 != 0) return fail(PGMI_E_ARG, "K must be a multiple of 8");
+    EpiArgs e{};
+    e.bias = reinterpret_cast<const uint16_t*>(bias);
+    e.res = reinterpret_cast<const uint16_t*>(res);
+    e.ldr = N;
+    e.ldo = N;
+    if (epi == EPI_F32) e.out_f32 = reinterpret_cast<float*>(out);
+    else e.out = reinterpret_cast<uint16_t*>(out);
+    gemm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(A), K, reinterpret_cast<const uint16_t*>(Wt), K, M, N,
+         K, (Epi)epi, e, x->ws, x->ws_bytes, epi == EPI_GEGLU ? N : 0);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_rmsnorm(pgmi_ctx* x, const void* in, const void* w, int rows, int D, float eps, void* out, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    rmsnorm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(w), eps,
+            reinterpret_cast<uint16_t*>(out), rows, D);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_layernorm(pgmi_ctx* x, const void* in, const void* w, const void* b, int rows, int D, float eps, void* out,
+                      void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    layernorm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(w),
+              reinterpret_cast<const uint16_t*>(b), eps, reinterpret_cast<uint16_t*>(out), rows, D);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_attention(pgmi_ctx* x, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk, int H,
+                      int Hkv, int hd, float scale, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (hd != 256 && hd != 72) return fail(PGMI_E_ARG, "head_dim must be 72 or 256");
+    if (H % Hkv != 0 || H / Hkv > 16) return fail(PGMI_E_ARG, "bad head grouping");
+    if (Lk > attention_prefill_max_keys(hd)) return fail(PGMI_E_ARG, "too many keys");
+    AttnArgs a{};
+    a.q = reinterpret_cast<const uint16_t*>(q); a.q_b_stride = (long)Lq * H * hd; a.q_row_stride = H * hd; a.q_head_stride = hd;
+    a.k = reinterpret_cast<const uint16_t*>(k); a.k_b_stride = (long)Lk * Hkv * hd; a.k_row_stride = Hkv * hd; a.k_head_stride = hd;
+    a.v = reinterpret_cast<const uint16_t*>(v); a.v_b_stride = a.k_b_stride; a.v_row_stride = Hkv * hd; a.v_head_stride = hd;
+    a.o = reinterpret_cast<uint16_t*>(o); a.o_b_stride = a.q_b_stride; a.o_row_stride = H * hd; a.o_head_stride = hd;
+    a.Lq = Lq; a.Lk = Lk; a.G = H / Hkv; a.n_kv = Hkv; a.B = B; a.scale = scale;
+    attention_prefill((hipStream_t)stream, hd, a);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_gemv_res(pgmi_ctx* x, const void* in, const void* Wt, int B, int N, int K, void* h, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (K != 2048 && K != 16384) return fail(PGMI_E_ARG, "K must be 2048 or 16384");
+    if (B < 1 || B > 8) return fail(PGMI_E_ARG, "B must be in [1, 8]");
+    gemv_res((hipStream_t)stream, B, K, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(Wt), N,
+             reinterpret_cast<uint16_t*>(h));
+    LAUNCHCHK();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,362 @@
+// kernels_gemv.hip -- KV-cached decode projections (batch B <= 8 rows), gfx950.
+//
+// Decode at batch 1 streams ~5.02 GB of weights per token, so every
+// projection of GemmaDecoderLayer (modeling_gemma.py:307-338) is one HBM-bound pass over
+// its nn.Linear weight [N][K] (K contiguous, used as stored):
+//   - each wave owns RPW "units" (1 row, or a row pair: RoPE's (d, d+128) or GeGLU's
+//     (gate n, up n)); lane l covers K elements [8l + 512c, +8) for c < K/512, so one
+//     wave-instruction reads 1 KiB contiguous of a row (16 B per lane, non-temporal);
+//   - the activation (B x K, bf16) is staged once per workgroup in LDS, with the
+//     preceding RMSNorm fused into that prologue (modeling_gemma.py:114-120);
+//   - the first unit group's weight loads are issued BEFORE the prologue, and the next
+//     group's before the current group's reduction/epilogue;
+//   - fp32 accumulation via v_dot2_f32_bf16, one wave reduction per output;
+//   - the reference's rounding points live in the epilogues (RoPE: modeling_gemma.py:
+//     197-198, KV append :259, residual :327/:336, GeGLU :134, logits :417-418).
+#include "common.h"
+#include "launch.h"
+
+namespace pgmi {
+
+enum GemvMode : int { GV_QKV = 0, GV_RES = 1, GV_GEGLU = 2, GV_LOGITS = 3 };
+
+struct GemvArgs {
+    const uint16_t* x;       // activation rows [nb][K] (h for the norm'd modes)
+    const uint16_t* norm_w;  // RMSNorm weight (nullptr: plain copy)
+    float eps;
+    const uint16_t* W;       // weight rows
+    int n_units;
+    int K;
+    int nb;                  // valid batch rows (<= template B)
+    int I;                   // GeGLU: up rows offset; QKV: number of q heads
+    // outputs
+    uint16_t* out;           // RES: h in/out [nb][N]; GEGLU: act [nb][I]; QKV: q [nb][nh*256]
+    float* logits;           // LOGITS: [nb][N]
+    float* pmax;             // LOGITS: per-block partial max [nb][gridDim]
+    int* pidx;
+    // QKV
+    const uint16_t* cosT;
+    const uint16_t* sinT;
+    int max_pos;
+    const StepState* st;
+    uint16_t* kc;
+    uint16_t* vc;
+    long kv_b_stride;
+    int nkv;
+};
+
+// WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their
+// partial sums meet in LDS; 4/WK unit groups per workgroup.
+template <int B, int KCH, int RPW, int MODE, int WK>
+__global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
+    constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
+    constexpr int KCW = KCH / WK;  // chunks per wave
+    constexpr int NL = RPW * NR * KCW;
+    constexpr int K = KCH * 512;
+    constexpr int GPB = 4 / WK;    // unit groups per block
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [B][K]
+    __shared__ float red[4][B];
+    __shared__ float kred[WK > 1 ? 4 : 1][RPW * NR * B];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wk = wave % WK, grp = wave / WK;
+    const int stride = gridDim.x * GPB * RPW;
+    int bb = blockIdx.x * GPB * RPW;  // block-uniform loop base
+    int ub = bb + grp * RPW;
+    const int kofs = wk * KCW * 512 + 8 * lane;
+
+    auto row_of = [&](int u, int j) -> long {
+        if constexpr (MODE == GV_QKV) return (long)((u >> 7) * 256 + (u & 127) + j * 128);
+        else if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
+        else return (long)u;
+    };
+
+    uint4 w[NL];
+    auto issue = [&](int base) {
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            int u = base + i;
+            if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate work, result discarded
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const uint16_t* rp = a.W + row_of(u, j) * K + kofs;
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) w[(i * NR + j) * KCW + c] = ldg_nt(rp + 512 * c);
+            }
+        }
+    };
+    if (ub < a.n_units) issue(ub);
+
+    // ---- prologue: stage (RMSNorm'd) activation rows in LDS
+    {
+        float ss[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) ss[b] = 0.f;
+        for (int c = tid * 8; c < K; c += 256 * 8) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                uint4 v = (b < a.nb) ? ldg16(a.x + (long)b * K + c) : make_uint4(0, 0, 0, 0);
+                *reinterpret_cast<uint4*>(xs + b * K + c) = v;
+                if (a.norm_w) {
+                    const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { float f = bf2f(e[j]); ss[b] += f * f; }
+                }
+            }
+        }
+        if (a.norm_w) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                float t = wave_sum(ss[b]);
+                if (lane == 0) red[wave][b] = t;
+            }
+            __syncthreads();
+            float r[B];
+#pragma unroll
+            for (int b = 0; b < B; ++b)
+                r[b] = 1.0f / sqrtf((red[0][b] + red[1][b] + red[2][b] + red[3][b]) / (float)K + a.eps);
+            for (int c = tid * 8; c < K; c += 256 * 8) {
+                uint4 wv = ldg16(a.norm_w + c);
+                const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    uint4 v = *reinterpret_cast<uint4*>(xs + b * K + c);
+                    const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+                    u16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r[b]) * (1.0f + bf2f(we[j])));
+                    *reinterpret_cast<u16x8*>(xs + b * K + c) = o;
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    int kv_len = 0, pos = 0;
+    if constexpr (MODE == GV_QKV) {
+        kv_len = a.st->kv_len;
+        pos = a.st->position;
+        if (pos < 0) pos = 0;
+        if (pos > a.max_pos - 1) pos = a.max_pos - 1;  // clamp (modeling_gemma.py:163-165)
+    }
+    float best[B];
+    int besti[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) { best[b] = -INFINITY; besti[b] = 0x7fffffff; }
+
+    while (bb < a.n_units) {
+        float acc[RPW][NR][B];
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int b = 0; b < B; ++b) acc[i][j][b] = 0.f;
+#pragma unroll
+        for (int c = 0; c < KCW; ++c) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint4 xv = *reinterpret_cast<const uint4*>(xs + b * K + kofs + 512 * c);
+#pragma unroll
+                for (int i = 0; i < RPW; ++i)
+#pragma unroll
+                    for (int j = 0; j < NR; ++j) acc[i][j][b] = dot8(w[(i * NR + j) * KCW + c], xv, acc[i][j][b]);
+            }
+        }
+        const int cur = ub;
+        ub += stride;
+        bb += stride;
+        if (ub < a.n_units) issue(ub);  // next group's stream starts before this group's epilogue
+
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int b = 0; b < B; ++b) acc[i][j][b] = wave_sum(acc[i][j][b]);
+        if constexpr (WK > 1) {
+            // combine the WK K-slices of each unit in a fixed order
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < RPW; ++i)
+#pragma unroll
+                    for (int j = 0; j < NR; ++j)
+#pragma unroll
+                        for (int b = 0; b < B; ++b) kred[wave][(i * NR + j) * B + b] = acc[i][j][b];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < RPW; ++i)
+#pragma unroll
+                for (int j = 0; j < NR; ++j)
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        float t = 0.f;
+#pragma unroll
+                        for (int q = 0; q < WK; ++q) t += kred[grp * WK + q][(i * NR + j) * B + b];
+                        acc[i][j][b] = t;
+                    }
+            __syncthreads();
+            if (wk != 0) continue;  // slice 0 of each group writes
+        }
+
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int u = cur + i;
+            if (u >= a.n_units) break;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                if (b >= a.nb) break;
+                if constexpr (MODE == GV_RES) {
+                    if (lane == 0) {
+                        uint16_t* hp = a.out + (long)b * a.n_units + u;
+                        *hp = f2bf(rbf(acc[i][0][b]) + bf2f(*hp));
+                    }
+                } else if constexpr (MODE == GV_GEGLU) {
+                    if (lane == 0) {
+                        const float g = rbf(gelu_tanh(rbf(acc[i][0][b])));
+                        a.out[(long)b * a.I + u] = f2bf(g * rbf(acc[i][1][b]));
+                    }
+                } else if constexpr (MODE == GV_LOGITS) {
+                    const float v = rbf(acc[i][0][b]);
+                    if (lane == 0) a.logits[(long)b * a.n_units + u] = v;
+                    if (v > best[b]) { best[b] = v; besti[b] = u; }  // rows visited in increasing order
+                } else {  // GV_QKV
+                    if (lane == 0) {
+                        const int hh = u >> 7, d = u & 127;
+                        const float x0 = rbf(acc[i][0][b]), x1 = rbf(acc[i][1][b]);
+                        const int nh = a.I;
+                        if (hh < nh + a.nkv) {
+                            const float c = bf2f(a.cosT[(long)pos * 128 + d]);
+                            const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
+                            const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
+                            const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sn));
+                            uint16_t* dst;
+                            if (hh < nh) {
+                                dst = a.out + (long)b * nh * 256 + hh * 256;
+                            } else {
+                                dst = a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
+                            }
+                            dst[d] = o0;
+                            dst[d + 128] = o1;
+                        } else {
+                            uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) +
+                                            (hh - nh - a.nkv) * 256;
+                            dst[d] = f2bf(x0);
+                            dst[d + 128] = f2bf(x1);
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    if constexpr (MODE == GV_LOGITS) {
+        // block-level first-max over the 4 waves, one partial per block
+        __shared__ float bv[4][B];
+        __shared__ int bi[4][B];
+        if (lane == 0) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) { bv[wave][b] = best[b]; bi[wave][b] = besti[b]; }
+        }
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                if (b >= a.nb) break;
+                float m = bv[0][b];
+                int mi = bi[0][b];
+                for (int q = 1; q < 4; ++q)
+                    if (bv[q][b] > m || (bv[q][b] == m && bi[q][b] < mi)) { m = bv[q][b]; mi = bi[q][b]; }
+                a.pmax[(long)b * gridDim.x + blockIdx.x] = m;
+                a.pidx[(long)b * gridDim.x + blockIdx.x] = mi;
+            }
+        }
+    }
+}
+
+template <int B, int KCH, int RPW, int MODE, int WK = 1>
+static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
+    const size_t lds = (size_t)B * KCH * 512 * sizeof(uint16_t);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    constexpr int per_block = (4 / WK) * RPW;
+    int blocks = (a.n_units + per_block - 1) / per_block;
+    if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK>), dim3(blocks), dim3(256), lds, s, a);
+}
+
+// K = 2048 (hidden); nh q heads, nkv kv heads of 256
+void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
+              const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride) {
+    GemvArgs a{};
+    a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wqkv; a.n_units = (nh + 2 * nkv) * 128; a.K = 2048; a.nb = B;
+    a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
+    a.kv_b_stride = kv_b_stride; a.nkv = nkv;
+#define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
+    if (B <= 1) L_(1, 4, 1, GV_QKV);
+    else if (B <= 2) L_(2, 4, 1, GV_QKV);
+    else if (B <= 4) L_(4, 4, 1, GV_QKV);
+    else L_(8, 4, 1, GV_QKV);
+}
+
+void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout) {
+    GemvArgs a{};
+    a.x = x; a.norm_w = nullptr; a.W = W; a.n_units = N; a.K = K; a.nb = B; a.out = h_inout;
+    if (K == 2048) {
+        if (B <= 1) L_(1, 4, 1, GV_RES);
+        else if (B <= 2) L_(2, 4, 1, GV_RES);
+        else if (B <= 4) L_(4, 4, 1, GV_RES);
+        else L_(8, 4, 1, GV_RES);
+    } else {  // K = 16384: x staged per <= 4 rows (LDS 32 KiB per row)
+        for (int b0 = 0; b0 < B; b0 += 4) {
+            const int nb = (B - b0) < 4 ? (B - b0) : 4;
+            GemvArgs c = a;
+            c.x = x + (long)b0 * K; c.out = h_inout + (long)b0 * N; c.nb = nb;
+            if (nb <= 1) launch_gemv<1, 32, 2, GV_RES, 4>(s, c);
+            else if (nb <= 2) launch_gemv<2, 32, 2, GV_RES, 4>(s, c);
+            else launch_gemv<4, 32, 2, GV_RES, 4>(s, c);
+        }
+    }
+}
+
+void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* Wgu,
+                int I, uint16_t* act) {
+    GemvArgs a{};
+    a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
+    if (B <= 1) L_(1, 4, 2, GV_GEGLU);
+    else if (B <= 2) L_(2, 4, 2, GV_GEGLU);
+    else if (B <= 4) L_(4, 4, 2, GV_GEGLU);
+    else L_(8, 4, 1, GV_GEGLU);
+}
+
+int gemv_logits_blocks() { return 2048; }
+
+void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
+                 int V, float* logits, float* pmax, int* pidx, int* nparts) {
+    GemvArgs a{};
+    a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
+    a.pmax = pmax; a.pidx = pidx;
+    const int mb = gemv_logits_blocks();
+    int blocks;
+#define LG_(b_, rpw)                                                    \
+    do {                                                                \
+        blocks = (V + 4 * rpw - 1) / (4 * rpw);                         \
+        if (blocks > mb) blocks = mb;                                   \
+        launch_gemv<b_, 4, rpw, GV_LOGITS>(s, a, mb);                   \
+    } while (0)
+    if (B <= 1) LG_(1, 4);
+    else if (B <= 2) LG_(2, 4);
+    else if (B <= 4) LG_(4, 2);
+    else LG_(8, 2);
+    *nparts = blocks;
+#undef LG_
+#undef L_
+}
+
+}  // namespace pgmi

@@ -1,0 +1,96 @@
+// launch.h -- host-side launchers for the libpgmi kernels (internal, not the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pgmi {
+
+// ---------------------------------------------------------------- GEMM (prefill)
+enum Epi : int {
+    EPI_STORE = 0,      // out = bf16(acc)
+    EPI_BIAS = 1,       // out = bf16(acc + bias)
+    EPI_BIAS_GELU = 2,  // out = bf16(gelu(bf16(acc + bias)))
+    EPI_BIAS_RES = 3,   // out = bf16(bf16(acc + bias) + res)
+    EPI_RES = 4,        // out = bf16(bf16(acc) + res)
+    EPI_BIAS_POS = 5,   // out = bf16(bf16(acc + bias) + pos[m % npos])
+    EPI_F32 = 6,        // out_f32 = float(bf16(acc))
+    EPI_GEGLU = 7,      // out = bf16(bf16(gelu(bf16(acc_gate))) * bf16(acc_up))  (dual B)
+};
+
+struct EpiArgs {
+    const uint16_t* bias = nullptr;
+    const uint16_t* res = nullptr;  // [M][ldr]
+    int ldr = 0;
+    const uint16_t* pos = nullptr;  // [npos][N]
+    int npos = 0;
+    uint16_t* out = nullptr;        // [M][ldo]
+    int ldo = 0;
+    float* out_f32 = nullptr;       // [M][ldo]
+};
+
+// C[M,N] = A[M,K] (row-major, lda) x W[N,K]^T (row-major, ldw).  For EPI_GEGLU the
+// "up" weight rows are W + up_offset_rows*ldw.  `ws` is fp32 scratch for split-K.
+void gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+          Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0);
+size_t gemm_ws_bytes(int M, int N, int K);
+
+// ---------------------------------------------------------------- decode GEMV
+struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)
+    int kv_len;     // index the new token's K/V is written at (= KVCache.num_items())
+    int position;   // rotary position (= attention_mask.cumsum(-1)[:, -1], modeling_gemma.py:526)
+};
+
+// fused input RMSNorm + q/k/v projection + RoPE + KV-cache append (K = 2048)
+void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
+              const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride);
+void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout);
+void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
+                const uint16_t* Wgu, int I, uint16_t* act);
+int gemv_logits_blocks();
+void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
+                 const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts);
+void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out);
+void argmax_rows(hipStream_t s, const float* x, int rows, int V, int64_t* out);
+
+// ---------------------------------------------------------------- attention
+struct AttnArgs {
+    const uint16_t* q; long q_b_stride; int q_row_stride; int q_head_stride;
+    const uint16_t* k; long k_b_stride; int k_row_stride; int k_head_stride;
+    const uint16_t* v; long v_b_stride; int v_row_stride; int v_head_stride;
+    uint16_t* o; long o_b_stride; int o_row_stride; int o_head_stride;
+    int Lq;        // query positions per batch element
+    int Lk;        // keys
+    int G;         // query heads per kv head
+    int n_kv;      // kv heads
+    int B;
+    float scale;   // s = bf16(bf16(q.k) * scale)
+};
+void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
+// decode: Lq == 1, rows = the G heads; keys split over chunks; kv length from StepState (+1)
+// max_keys = allocated key stride of `scores`; launch_keys = upper bound on kv_len+1 this call
+void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int max_keys, int launch_keys,
+                      float* scores, float* opart, int max_chunks);
+int attention_prefill_max_keys(int head_dim);
+
+// ---------------------------------------------------------------- misc
+void rmsnorm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, uint16_t* out, int rows, int D);
+void layernorm(hipStream_t s, const uint16_t* x, const uint16_t* w, const uint16_t* b, float eps, uint16_t* out,
+               int rows, int D);
+void embed_rows(hipStream_t s, const int64_t* ids, int rows, const uint16_t* E, int D, float normalizer,
+                int64_t pad_id, uint16_t* out);
+// merge (modeling_gemma.py:468-537) + GemmaModel normalizer (:367-368)
+void merge_embed(hipStream_t s, const int64_t* ids, int B, int L, const uint16_t* E, int D,
+                 const uint16_t* img, int n_img_rows, int64_t image_token, int64_t pad_id, float sqrt_h,
+                 float normalizer, const uint16_t* embeds_in, int* scan_buf, uint16_t* out);
+void scale_rows(hipStream_t s, const uint16_t* x, long n, float normalizer, uint16_t* out);
+void rope_kv_append(hipStream_t s, const uint16_t* qkv, int B, int L, int nh, int nkv, const int64_t* pos,
+                    const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out, uint16_t* kcache,
+                    uint16_t* vcache, long kv_b_stride, int kv_start);
+void patchify(hipStream_t s, const void* px, int px_is_f32, int B, int C, int H, int W, int P, int Kpad,
+              uint16_t* out);
+void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float scale, float offset);
+void set_step(hipStream_t s, StepState* st, int kv_len, int position);
+void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uint16_t* dst);
+
+}  // namespace pgmi

@@ -1,0 +1,244 @@
+"""Engine: one libpgmi context on one GPU (weights slab, KV slabs, forward calls).
+
+Device memory for the weights and the KV caches is torch-allocated (so the Python API can
+expose the reference's parameter / cache tensors as views of it); the library owns its
+workspaces.  Every compute call goes through libpgmi.so -- nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional
+
+import torch
+
+from . import _native as N
+
+
+def config_dict(cfg) -> dict:
+    """Accept a PaliGemmaConfig (reference or drop-in) or an HF-style config.json dict."""
+    if isinstance(cfg, dict):
+        v, t = dict(cfg["vision_config"]), dict(cfg["text_config"])
+        top = cfg
+        get = top.get
+    else:
+        v = dict(vars(cfg.vision_config))
+        t = dict(vars(cfg.text_config))
+        top = vars(cfg)
+        get = top.get
+    pad = get("pad_token_id", None)
+    return {
+        "v_hidden": v.get("hidden_size", 768), "v_intermediate": v.get("intermediate_size", 3072),
+        "v_layers": v.get("num_hidden_layers", 12), "v_heads": v.get("num_attention_heads", 12),
+        "v_channels": v.get("num_channels", 3), "v_image": v.get("image_size", 224),
+        "v_patch": v.get("patch_size", 16), "v_ln_eps": v.get("layer_norm_eps", 1e-6),
+        "t_vocab": t["vocab_size"], "t_hidden": t["hidden_size"], "t_intermediate": t["intermediate_size"],
+        "t_layers": t["num_hidden_layers"], "t_heads": t["num_attention_heads"],
+        "t_kv_heads": t["num_key_value_heads"], "t_head_dim": t.get("head_dim", 256),
+        "t_max_pos": t.get("max_position_embeddings", 8192), "t_rms_eps": t.get("rms_norm_eps", 1e-6),
+        "t_rope_theta": t.get("rope_theta", 10000.0),
+        "projection_dim": get("projection_dim", 2048), "image_token_index": get("image_token_index", 256000),
+        "pad_token_id": -1 if pad is None else int(pad),
+        "hidden_size": get("hidden_size", 2048),
+    }
+
+
+class Engine:
+    def __init__(self, cfg, device=None, max_batch: int = 8, max_seq: int = 1472, max_kv: Optional[int] = None):
+        self.lib = N.lib()
+        self.cfgd = config_dict(cfg)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        c = N.PgmiConfig()
+        for k, _ in N.PgmiConfig._fields_:
+            if k in ("max_batch", "max_seq", "max_kv"):
+                continue
+            setattr(c, k, self.cfgd[k])
+        c.max_batch, c.max_seq = max_batch, max_seq
+        c.max_kv = max_kv if max_kv else self.cfgd["t_max_pos"]
+        self.max_batch, self.max_seq, self.max_kv = max_batch, max_seq, c.max_kv
+        h = ctypes.c_void_p()
+        N.check(self.lib.pgmi_create(self.device.index, ctypes.byref(c), ctypes.byref(h)), "pgmi_create")
+        self.ctx = h
+        nbytes = self.lib.pgmi_weights_bytes(self.ctx)
+        self.slab = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        N.check(self.lib.pgmi_bind_weights(self.ctx, self.slab.data_ptr()), "pgmi_bind_weights")
+        self.views = {}
+        for i in range(self.lib.pgmi_weight_count(self.ctx)):
+            name, off, shape, nd = ctypes.c_char_p(), ctypes.c_int64(), (ctypes.c_int64 * 4)(), ctypes.c_int()
+            N.check(self.lib.pgmi_weight_info(self.ctx, i, ctypes.byref(name), ctypes.byref(off),
+                                              ctypes.byref(shape), ctypes.byref(nd)))
+            shp = tuple(shape[j] for j in range(nd.value))
+            numel = math.prod(shp)
+            self.views[name.value.decode()] = self.slab[off.value: off.value + 2 * numel].view(torch.bfloat16).view(shp)
+        self.prepared = False
+        self._logits_buf = {}
+
+    def __del__(self):
+        try:
+            if getattr(self, "ctx", None):
+                self.lib.pgmi_destroy(self.ctx)
+                self.ctx = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ weights
+    def names(self):
+        return list(self.views.keys())
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: dict, strict: bool = True):
+        missing = [n for n in self.views if n not in sd]
+        if strict and missing:
+            raise KeyError(f"missing weights: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+        for n, view in self.views.items():
+            if n in sd:
+                t = sd[n]
+                if tuple(t.shape) != tuple(view.shape):
+                    raise ValueError(f"{n}: shape {tuple(t.shape)} != {tuple(view.shape)}")
+                view.copy_(t.to(device=self.device, dtype=torch.bfloat16))
+        self.prepared = False
+
+    def fill_synthetic(self, seed: int, policy):
+        """Device-side deterministic init (oracle/wgen.c recipe); policy(name, shape) -> (scale, offset)."""
+        s = N.stream_handle(self.device)
+        for n, view in self.views.items():
+            scale, offset = policy(n, tuple(view.shape))
+            key = self.lib.pgmi_synthetic_key(n.encode(), seed)
+            N.check(self.lib.pgmi_fill_synthetic(self.ctx, n.encode(), key, scale, offset, s), n)
+        self.prepared = False
+
+    def prepare(self, inv_freq: Optional[torch.Tensor] = None, exact_table: bool = True):
+        """RoPE tables from the module's inv_freq buffer (the reference's own values) and the
+        padded patch matrix.  With exact_table the cos/sin table is computed by torch on the
+        CPU exactly as GemmaRotaryEmbedding.forward does (modeling_gemma.py:168-185)."""
+        hd, mp = self.cfgd["t_head_dim"], self.cfgd["t_max_pos"]
+        if inv_freq is None:
+            inv_freq = 1.0 / (self.cfgd["t_rope_theta"] ** (torch.arange(0, hd, 2, dtype=torch.int64).float() / hd))
+        inv = inv_freq.detach().float().cpu().contiguous()
+        N.check(self.lib.pgmi_set_rope_inv_freq(self.ctx, inv.numpy().ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        if exact_table:
+            pos = torch.arange(mp, dtype=torch.float32)
+            freqs = (inv[None, :, None] @ pos[None, None, :]).transpose(1, 2)[0]  # (mp, hd/2) as :178
+            cos = freqs.cos().to(torch.bfloat16).contiguous().view(torch.int16)
+            sin = freqs.sin().to(torch.bfloat16).contiguous().view(torch.int16)
+            N.check(self.lib.pgmi_set_rope_table(self.ctx, cos.data_ptr(), sin.data_ptr(), mp))
+        N.check(self.lib.pgmi_prepare(self.ctx), "pgmi_prepare")
+        self.prepared = True
+
+    # ------------------------------------------------------------------ caches
+    def new_kv(self, batch: int, max_tokens: Optional[int] = None) -> torch.Tensor:
+        T = max_tokens or self.max_kv
+        t = self.cfgd
+        return torch.empty((t["t_layers"], 2, batch, T, t["t_kv_heads"] * t["t_head_dim"]),
+                           dtype=torch.bfloat16, device=self.device)
+
+    # ------------------------------------------------------------------ forward pieces
+    def _s(self):
+        return N.stream_handle(self.device)
+
+    def _ready(self):
+        if not self.prepared:
+            self.prepare()
+
+    def vision(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        self._ready()
+        px = pixel_values.to(self.device)
+        if px.dtype not in (torch.float32, torch.bfloat16):
+            px = px.float()
+        px = px.contiguous()
+        B = px.shape[0]
+        c = self.cfgd
+        n = (c["v_image"] // c["v_patch"]) ** 2
+        if tuple(px.shape[1:]) != (c["v_channels"], c["v_image"], c["v_image"]):
+            raise ValueError(f"pixel_values shape {tuple(px.shape)} does not match the vision config")
+        out = torch.empty((B, n, c["v_hidden"]), dtype=torch.bfloat16, device=self.device)
+        dt = N.DTYPE_F32 if px.dtype == torch.float32 else N.DTYPE_BF16
+        N.check(self.lib.pgmi_vision(self.ctx, px.data_ptr(), dt, B, out.data_ptr(), self._s()), "pgmi_vision")
+        return out
+
+    def project(self, feats: torch.Tensor) -> torch.Tensor:
+        self._ready()
+        f = feats.to(self.device, torch.bfloat16).contiguous()
+        rows = f.numel() // f.shape[-1]
+        out = torch.empty(f.shape[:-1] + (self.cfgd["projection_dim"],), dtype=torch.bfloat16, device=self.device)
+        N.check(self.lib.pgmi_project(self.ctx, f.data_ptr(), rows, out.data_ptr(), self._s()), "pgmi_project")
+        return out
+
+    def embed(self, ids: torch.Tensor) -> torch.Tensor:
+        self._ready()
+        i = ids.to(self.device, torch.int64).contiguous()
+        out = torch.empty(tuple(i.shape) + (self.cfgd["t_hidden"],), dtype=torch.bfloat16, device=self.device)
+        N.check(self.lib.pgmi_embed(self.ctx, i.data_ptr(), i.numel(), out.data_ptr(), self._s()), "pgmi_embed")
+        return out
+
+    def lm_forward(self, kv: torch.Tensor, kv_start: int, positions, ids=None, image_feats=None, embeds=None,
+                   logits_rows: int = 0) -> torch.Tensor:
+        """GemmaForCausalLM.forward over merged embeddings (see pgmi.h).  Returns fp32 logits
+        (B, L, V) or (B, 1, V)."""
+        self._ready()
+        if embeds is not None:
+            e = embeds.to(self.device, torch.bfloat16).contiguous()
+            B, L = e.shape[0], e.shape[1]
+            idp, imgp, nimg = None, None, 0
+        else:
+            ids = ids.to(self.device, torch.int64).contiguous()
+            B, L = ids.shape
+            e = None
+            idp = ids.data_ptr()
+            if image_feats is not None:
+                image_feats = image_feats.to(self.device, torch.bfloat16).contiguous()
+                imgp, nimg = image_feats.data_ptr(), image_feats.numel() // image_feats.shape[-1]
+            else:
+                imgp, nimg = None, 0
+        pos = torch.as_tensor(positions, dtype=torch.int64).cpu()
+        pos = torch.broadcast_to(pos.reshape(pos.shape[0] if pos.dim() > 1 else 1, -1), (B, L)).contiguous()
+        V = self.cfgd["t_vocab"]
+        out = torch.empty((B, L if logits_rows == 0 else 1, V), dtype=torch.float32, device=self.device)
+        N.check(self.lib.pgmi_lm_forward(self.ctx, idp, imgp, nimg, N.ptr(e), B, L, pos.data_ptr(), kv.data_ptr(),
+                                         kv.shape[2], kv.shape[3], kv_start, out.data_ptr(), logits_rows, self._s()),
+                "pgmi_lm_forward")
+        return out
+
+    def decode(self, ids: torch.Tensor, kv: torch.Tensor, kv_len: int, position: int, logits: torch.Tensor = None,
+               next_ids: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
+        """One KV-cached decode step for B sequences; returns logits (B, V) fp32."""
+        self._ready()
+        ids = ids.to(self.device, torch.int64).reshape(-1).contiguous()
+        B = ids.numel()
+        if logits is None:
+            logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        N.check(self.lib.pgmi_decode(self.ctx, ids.data_ptr(), B, kv.data_ptr(), kv.shape[2], kv.shape[3], kv_len,
+                                     position, logits.data_ptr(), N.ptr(next_ids), int(graph), self._s()),
+                "pgmi_decode")
+        return logits
+
+    def argmax(self, logits: torch.Tensor) -> torch.Tensor:
+        l2 = logits.reshape(-1, logits.shape[-1]).contiguous()
+        out = torch.empty(l2.shape[0], dtype=torch.int64, device=self.device)
+        N.check(self.lib.pgmi_argmax(self.ctx, l2.data_ptr(), l2.shape[0], l2.shape[1], out.data_ptr(), self._s()))
+        return out
+
+    # ------------------------------------------------------------------ batched greedy driver
+    @torch.no_grad()
+    def generate(self, input_ids: torch.Tensor, pixel_values: torch.Tensor, n_tokens: int, graph: bool = True,
+                 kv: torch.Tensor = None):
+        """Batched greedy generation: prefill, then n_tokens-1 decode
+        steps with device-side argmax and no host sync per token.  Positions follow
+        inference.py's semantics (first decode position = L + 1, modeling_gemma.py:526)."""
+        ids = input_ids.to(self.device, torch.int64)
+        B, L = ids.shape
+        if kv is None:
+            kv = self.new_kv(B, L + n_tokens + 1)
+        feats = self.project(self.vision(pixel_values))
+        logits = self.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=1)
+        toks = torch.empty((B, n_tokens), dtype=torch.int64, device=self.device)
+        toks[:, 0] = self.argmax(logits[:, 0])
+        step_logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        nxt = torch.empty(B, dtype=torch.int64, device=self.device)
+        cur = toks[:, 0].clone()
+        for t in range(1, n_tokens):
+            self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=nxt, graph=graph)
+            toks[:, t] = nxt
+            cur.copy_(nxt)
+        return toks

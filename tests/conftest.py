@@ -1,0 +1,22 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "multimodal-financial-analysis-tool-using-paligemma_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libpgmi.so)")
+    config.addinivalue_line("markers", "slow: full PaliGemma-3B shapes")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

@@ -1,0 +1,96 @@
+"""Model-level parity on the 2+2-layer full-width config: libpgmi (Engine) vs the golden
+vectors captured from the reference modules (tests/golden/small_bf16.npz) and vs the oracle
+run here on the same synthetic weights."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import paligemma_np as O
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+SEED = 1234
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def gold(golden_dir):
+    return np.load(os.path.join(golden_dir, "small_bf16.npz"))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from pgmi import Engine
+    cfg = W.small_config()
+    e = Engine(cfg, max_batch=4, max_seq=640, max_kv=1024)
+    e.fill_synthetic(SEED, W.init_policy)
+    e.prepare()
+    return e
+
+
+def tap(gold, name):
+    return O.from_bits(gold["tap_" + name])
+
+
+def test_vision_tower(eng, gold):
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    feats = eng.vision(px).float().cpu().numpy()
+    assert rel_l2(feats[:, ::8], tap(gold, "vision_out")) < 1e-2
+    proj = eng.project(eng.vision(px)).float().cpu().numpy()
+    assert rel_l2(proj[:, ::8], tap(gold, "image_features")) < 1.5e-2
+
+
+def test_prefill_logits(eng, gold):
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    L = ids.shape[1]
+    kv = eng.new_kv(1, 1024)
+    feats = eng.project(eng.vision(px))
+    logits = eng.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=0)
+    torch.cuda.synchronize()
+    lg = logits.cpu().numpy()
+    ref_last = gold["prefill_logits_last"]
+    assert rel_l2(lg[:, -1], ref_last) < 3e-2
+    assert rel_l2(lg[:, ::32], O.from_bits(gold["prefill_logits_rows"])) < 3e-2
+    # last-row-only mode (decode GEMV kernel) gives the same numbers up to reassociation
+    kv2 = eng.new_kv(1, 1024)
+    last = eng.lm_forward(kv2, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)
+    assert rel_l2(last.cpu().numpy()[:, 0], lg[:, -1]) < 1e-3  # GEMV vs GEMM accumulation order
+    # KV cache rows vs the reference's KVCache (layer 0 and last; every 4th row)
+    k0 = kv[0, 0, 0, :L].float().cpu().numpy()[::4]
+    assert rel_l2(k0, O.from_bits(gold["k0"])[0, 0]) < 1e-2
+    vl = kv[-1, 1, 0, :L].float().cpu().numpy()[::4]
+    assert rel_l2(vl, O.from_bits(gold["v_last"])[0, 0]) < 3e-2
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_greedy_tokens(eng, gold, graph):
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    toks = eng.generate(ids, px, 16, graph=graph).cpu().numpy()
+    ref = gold["greedy_tokens"].reshape(1, -1)
+    # margins of the reference's own greedy choices: a step whose top-2 margin is below
+    # 0.25 may legitimately flip under bf16 reassociation
+    rl = O.from_bits(gold["greedy_logits"])
+    s = np.sort(rl, -1)
+    margin = s[:, -1] - s[:, -2]
+    first_diff = int(np.argmax(toks[0] != ref[0])) if (toks[0] != ref[0]).any() else None
+    if first_diff is not None:
+        assert margin[first_diff] < 0.25, (toks, ref, margin)
+
+
+def test_batched_decode_matches_single(eng, gold):
+    """B=3 lock-step decode (new capability): each row equals the B=1 run of that image."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    pxs = torch.stack([px[0], px[0].flip(-1), px[0].flip(-2)])
+    ids = torch.from_numpy(gold["ids"]).cuda().expand(3, -1).contiguous()
+    tb = eng.generate(ids, pxs, 6, graph=False).cpu().numpy()
+    for i in range(3):
+        t1 = eng.generate(ids[i:i + 1], pxs[i:i + 1], 6, graph=False).cpu().numpy()
+        assert np.array_equal(tb[i], t1[0]), (i, tb[i], t1[0])

@@ -1,0 +1,185 @@
+"""Kernel-level parity: each libpgmi op (through the C ABI) vs the CPU restatement in
+oracle/paligemma_np.py on the same seeded inputs.
+
+Tolerances: elementwise ops within 2 bf16 ulp; GEMM / attention rel-L2
+<= 1e-2 (in practice ~1e-3: both sides accumulate in fp32, only the order differs)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import paligemma_np as O
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+def bf(x_np):
+    """numpy float32 (bf16-valued) -> cuda bf16 tensor."""
+    return torch.from_numpy(O.bf16(x_np)).to(torch.bfloat16).cuda()
+
+
+def np32(t):
+    return t.detach().float().cpu().numpy()
+
+
+def rand(rng, *shape, scale=1.0):
+    return O.bf16(rng.standard_normal(shape).astype(np.float32) * np.float32(scale))
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def ulp_frac(a, b, ulps=1):
+    """fraction of elements within `ulps` bf16 ulps of each other"""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    sp = np.abs(b) * np.float32(2.0 ** -7) + np.float32(1e-30)
+    return float((np.abs(a - b) <= ulps * sp).mean())
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from pgmi import Engine
+    cfg = W.small_config(vision_layers=1, text_layers=1, vocab=1024)
+    e = Engine(cfg, max_batch=2, max_seq=320, max_kv=1024)
+    e.fill_synthetic(1234, W.init_policy)
+    e.prepare()
+    return e
+
+
+def _gemm(eng, A, Wt, epi, bias=None, res=None, out_f32=False, geglu=False):
+    M, K = A.shape
+    N = Wt.shape[0] // (2 if geglu else 1)
+    out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device="cuda")
+    from pgmi import _native as NN
+    NN.check(eng.lib.pgmi_op_gemm(eng.ctx, A.data_ptr(), Wt.data_ptr(), M, N, K, epi,
+                                  NN.ptr(bias), NN.ptr(res), out.data_ptr(), NN.stream_handle()))
+    torch.cuda.synchronize()
+    return np32(out)
+
+
+@pytest.mark.parametrize("M,N,K", [(288, 2560, 2048), (256, 4304, 1152), (256, 1152, 4304), (288, 2048, 16384),
+                                   (37, 200, 64), (1, 128, 2048), (256, 1152, 640)])
+def test_gemm_store(eng, M, N, K):
+    rng = np.random.default_rng(M * 7 + N + K)
+    A, Wt = rand(rng, M, K), rand(rng, N, K, scale=1 / np.sqrt(K))
+    got = _gemm(eng, bf(A), bf(Wt), 0)
+    ref = O.bf16(A @ Wt.T)
+    assert rel_l2(got, ref) < 2e-3
+    assert ulp_frac(got, ref, 1) > 0.99
+
+
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_res", "res", "f32"])
+def test_gemm_epilogues(eng, epi):
+    from pgmi._native import EPI
+    rng = np.random.default_rng(5)
+    M, N, K = 256, 1152, 1152
+    A, Wt = rand(rng, M, K), rand(rng, N, K, scale=1 / np.sqrt(K))
+    b, r = rand(rng, N, scale=0.1), rand(rng, M, N)
+    acc = A @ Wt.T
+    if epi == "bias":
+        ref = O.bf16(acc + b)
+    elif epi == "bias_gelu":
+        ref = O.gelu_tanh(O.bf16(acc + b))
+    elif epi == "bias_res":
+        ref = O.bf16(O.bf16(acc + b) + r)
+    elif epi == "res":
+        ref = O.bf16(O.bf16(acc) + r)
+    else:
+        ref = O.bf16(acc)
+    got = _gemm(eng, bf(A), bf(Wt), EPI[epi], bias=bf(b), res=bf(r), out_f32=(epi == "f32"))
+    assert rel_l2(got, ref) < 3e-3
+    assert ulp_frac(got, ref, 1) > 0.98
+
+
+def test_gemm_geglu(eng):
+    rng = np.random.default_rng(9)
+    M, N, K = 288, 512, 2048
+    A = rand(rng, M, K)
+    Wg, Wu = rand(rng, N, K, scale=2 / np.sqrt(K)), rand(rng, N, K, scale=2 / np.sqrt(K))
+    got = _gemm(eng, bf(A), bf(np.concatenate([Wg, Wu])), 7, geglu=True)
+    ref = O.bf16(O.gelu_tanh(O.bf16(A @ Wg.T)) * O.bf16(A @ Wu.T))
+    assert rel_l2(got, ref) < 5e-3
+
+
+def test_rmsnorm(eng):
+    from pgmi import _native as NN
+    rng = np.random.default_rng(3)
+    x, w = rand(rng, 300, 2048, scale=3.0), rand(rng, 2048, scale=0.1)
+    out = torch.empty((300, 2048), dtype=torch.bfloat16, device="cuda")
+    xt, wt = bf(x), bf(w)  # keep the inputs alive across the call
+    NN.check(eng.lib.pgmi_op_rmsnorm(eng.ctx, xt.data_ptr(), wt.data_ptr(), 300, 2048, 1e-6, out.data_ptr(),
+                                     NN.stream_handle()))
+    torch.cuda.synchronize()
+    ref = O.rms_norm(x, w, 1e-6)
+    assert ulp_frac(np32(out), ref, 2) == 1.0
+
+
+def test_layernorm(eng):
+    from pgmi import _native as NN
+    rng = np.random.default_rng(4)
+    x, w, b = rand(rng, 256, 1152, scale=2.0), O.bf16(1 + rand(rng, 1152, scale=0.1)), rand(rng, 1152, scale=0.05)
+    out = torch.empty((256, 1152), dtype=torch.bfloat16, device="cuda")
+    xt, wt, bt = bf(x), bf(w), bf(b)
+    NN.check(eng.lib.pgmi_op_layernorm(eng.ctx, xt.data_ptr(), wt.data_ptr(), bt.data_ptr(), 256, 1152,
+                                       1e-6, out.data_ptr(), NN.stream_handle()))
+    torch.cuda.synchronize()
+    ref = O.layer_norm(x, w, b, 1e-6)
+    assert ulp_frac(np32(out), ref, 2) > 0.999
+
+
+def _attn_ref(q, k, v, scale):
+    # q (B,Lq,H,d), k/v (B,Lk,Hkv,d)
+    H, Hkv = q.shape[2], k.shape[2]
+    qh = q.transpose(0, 2, 1, 3)
+    kh = np.repeat(k.transpose(0, 2, 1, 3), H // Hkv, axis=1)
+    vh = np.repeat(v.transpose(0, 2, 1, 3), H // Hkv, axis=1)
+    s = O.bf16(O.bf16(qh @ kh.transpose(0, 1, 3, 2)) * np.float32(scale))
+    p = O.bf16(O.softmax_f32(s))
+    return O.bf16(p @ vh).transpose(0, 2, 1, 3)
+
+
+@pytest.mark.parametrize("B,Lq,Lk,H,Hkv,d,scale", [
+    (1, 256, 256, 16, 16, 72, 72 ** -0.5),     # SigLIP 224
+    (2, 100, 100, 16, 16, 72, 72 ** -0.5),
+    (1, 288, 288, 8, 1, 256, 1 / 16),          # Gemma prefill (MQA)
+    (2, 33, 70, 8, 1, 256, 1 / 16),            # ragged, keys beyond queries (cache)
+    (1, 1, 290, 8, 1, 256, 1 / 16),            # one query position
+])
+def test_attention_prefill(eng, B, Lq, Lk, H, Hkv, d, scale):
+    from pgmi import _native as NN
+    rng = np.random.default_rng(Lq + Lk + d)
+    q, k, v = rand(rng, B, Lq, H, d, scale=2.0), rand(rng, B, Lk, Hkv, d, scale=2.0), rand(rng, B, Lk, Hkv, d)
+    o = torch.empty((B, Lq, H, d), dtype=torch.bfloat16, device="cuda")
+    qt, kt, vt = bf(q), bf(k), bf(v)
+    NN.check(eng.lib.pgmi_op_attention(eng.ctx, qt.data_ptr(), kt.data_ptr(), vt.data_ptr(), o.data_ptr(),
+                                       B, Lq, Lk, H, Hkv, d, scale, NN.stream_handle()))
+    torch.cuda.synchronize()
+    ref = _attn_ref(q, k, v, scale)
+    assert rel_l2(np32(o), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,K,N", [(1, 2048, 2048), (3, 2048, 2048), (1, 16384, 2048), (4, 16384, 2048),
+                                   (8, 2048, 1000), (6, 16384, 512)])
+def test_gemv_res(eng, B, K, N):
+    from pgmi import _native as NN
+    rng = np.random.default_rng(B * K + N)
+    x, Wt, h = rand(rng, B, K), rand(rng, N, K, scale=1 / np.sqrt(K)), rand(rng, B, N)
+    ht, xt, wt = bf(h), bf(x), bf(Wt)
+    NN.check(eng.lib.pgmi_op_gemv_res(eng.ctx, xt.data_ptr(), wt.data_ptr(), B, N, K, ht.data_ptr(),
+                                      NN.stream_handle()))
+    torch.cuda.synchronize()
+    ref = O.bf16(O.bf16(x @ Wt.T) + h)
+    assert rel_l2(np32(ht), ref) < 2e-3
+    assert ulp_frac(np32(ht), ref, 1) > 0.99
+
+
+def test_synthetic_fill_matches_oracle(eng):
+    """device generator (csrc/kernels_misc.hip) == oracle/wgen.c, bit for bit"""
+    for name, view in list(eng.views.items())[:12] + list(eng.views.items())[-6:]:
+        ref = W.gen_bf16(name, tuple(view.shape), 1234)
+        got = view.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+        assert np.array_equal(got, ref), name

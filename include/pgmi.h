@@ -120,6 +120,11 @@ int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch
 /* torch.argmax(logits, -1) over rows of a device fp32 [rows][V] matrix (inference.py:68) */
 int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* out, void* stream);
 
+/* Launch one decode kernel of `layer` on the context's decode workspace (benchmarking the
+ * dominant kernel in isolation): 1 o_proj+residual, 2 RMSNorm+gate/up+GeGLU, 3 down+residual,
+ * 4 final norm + lm_head (+argmax partials; layer ignored). */
+int pgmi_decode_kernel(pgmi_ctx* ctx, int which, int layer, int B, void* stream);
+
 /* ---- single-op entry points (kernel-level parity tests) ---------------------------------- */
 /* out = epilogue(A[M,K] . W[N,K]^T): epi 0 store, 1 +bias, 2 +bias,gelu, 3 +bias,+res, 4 +res,
  * 6 fp32 out (out is float*), 7 GeGLU with up rows at W + N*K */

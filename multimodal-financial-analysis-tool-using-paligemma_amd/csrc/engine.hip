@@ -89,7 +89,7 @@ struct pgmi_ctx {
     size_t ws_bytes;
     // decode workspace
     uint16_t *dH, *dQ, *dAO, *dACT;
-    float *scores, *opart, *pmax;
+    float *opart, *pmax, *dlogits;
     int* pidx;
     int max_chunks;
     StepState* step;
@@ -256,7 +256,8 @@ int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
     if (c.t_hidden != 2048) return fail(PGMI_E_ARG, "text hidden must be 2048 (decode kernels are specialised)");
     if (c.t_intermediate % 8 != 0 || c.v_intermediate % 8 != 0) return fail(PGMI_E_ARG, "intermediate sizes must be multiples of 8");
     if (c.v_hidden % c.v_heads != 0 || c.v_hidden / c.v_heads != 72) return fail(PGMI_E_ARG, "SigLIP head_dim must be 72");
-    if (c.t_heads % c.t_kv_heads != 0 || c.t_heads / c.t_kv_heads > 16) return fail(PGMI_E_ARG, "at most 16 query heads per kv head");
+    if (c.t_kv_heads != 1 || c.t_heads > 8)
+        return fail(PGMI_E_ARG, "decode path is specialised for MQA with <= 8 query heads (num_key_value_heads = 1)");
     if (c.max_batch < 1 || c.max_batch > 8) return fail(PGMI_E_ARG, "max_batch must be in [1, 8]");
     if (c.v_hidden > 4096) return fail(PGMI_E_ARG, "v_hidden too large for the LayerNorm kernel");
     auto* x = new pgmi_ctx();
@@ -407,9 +408,9 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->dAO, (size_t)B * H))) return rc;
         if ((rc = dalloc_t(x, &x->dACT, (size_t)B * c.t_intermediate))) return rc;
         x->max_chunks = (c.max_kv + 63) / 64;
-        if ((rc = dalloc_t(x, &x->scores, (size_t)B * c.t_kv_heads * 16 * c.max_kv))) return rc;
-        if ((rc = dalloc_t(x, &x->opart, (size_t)B * c.t_kv_heads * x->max_chunks * 16 * 256))) return rc;
+        if ((rc = dalloc_t(x, &x->opart, attention_decode_part_floats(B, c.t_kv_heads, x->max_chunks)))) return rc;
         if ((rc = dalloc_t(x, &x->pmax, (size_t)B * gemv_logits_blocks()))) return rc;
+        if ((rc = dalloc_t(x, &x->dlogits, (size_t)B * c.t_vocab))) return rc;
         if ((rc = dalloc_t(x, &x->pidx, (size_t)B * gemv_logits_blocks()))) return rc;
         if ((rc = dalloc_t(x, &x->step, 1))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
@@ -612,8 +613,9 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         a.v = Vc; a.v_b_stride = kvb; a.v_row_stride = (int)kvd; a.v_head_stride = HD;
         a.o = x->dAO; a.o_b_stride = (long)H; a.o_row_stride = H; a.o_head_stride = HD;
         a.Lq = 1; a.Lk = 0; a.G = NH / NKV; a.n_kv = NKV; a.B = B; a.scale = 1.0f / std::sqrt((float)HD);
-        attention_decode(s, a, x->step, c.max_kv, launch_keys, x->scores, x->opart, x->max_chunks);
-        gemv_res(s, B, NH * HD, x->dAO, TL(x, i, "self_attn.o_proj.weight"), H, x->dH);
+        attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
+        gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
+                    nullptr);
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH);
@@ -666,6 +668,34 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
 int pgmi_argmax(pgmi_ctx* x, const float* logits, int rows, int V, int64_t* out, void* stream) {
     if (!x || !logits || !out) return fail(PGMI_E_ARG, "null argument");
     argmax_rows((hipStream_t)stream, logits, rows, V, out);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    const pgmi_config& c = x->c;
+    if (B < 1 || B > c.max_batch) return fail(PGMI_E_ARG, "batch exceeds max_batch");
+    if (layer < 0 || layer >= c.t_layers) return fail(PGMI_E_ARG, "layer out of range");
+    hipStream_t s = (hipStream_t)stream;
+    const float eps = c.t_rms_eps;
+    const int H = c.t_hidden;
+    switch (which) {
+        case 1: gemv_res(s, B, c.t_heads * c.t_head_dim, x->dAO, TL(x, layer, "self_attn.o_proj.weight"), H, x->dH); break;
+        case 2:
+            gemv_geglu(s, B, x->dH, TL(x, layer, "post_attention_layernorm.weight"), eps, TL(x, layer, "mlp.gate_proj.weight"),
+                       c.t_intermediate, x->dACT);
+            break;
+        case 3: gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, layer, "mlp.down_proj.weight"), H, x->dH); break;
+        case 4: {
+            int nparts = 0;
+            gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps,
+                        W(x, "language_model.model.embed_tokens.weight"), c.t_vocab, x->dlogits, x->pmax, x->pidx, &nparts);
+            break;
+        }
+        default: return fail(PGMI_E_ARG, "unknown kernel id");
+    }
     LAUNCHCHK();
     return 0;
 }

@@ -174,113 +174,121 @@ int attention_prefill_max_keys(int head_dim) {
 }
 
 // ================================================================ decode (Lq = 1)
+// Flash-decoding: workgroup c owns keys [64c, 64c+64) of one (b, kv head) for all G query
+// heads.  Scores are rounded exactly as the reference (bf16(bf16(q.k) * scale)); each chunk
+// writes (m_c, l_c = sum e^(s - m_c), O_c = sum e^(s - m_c) v) in fp32.  The combine
+// o = bf16(sum_c e^(m_c - M) O_c / sum_c e^(m_c - M) l_c), in a fixed chunk order, is the
+// prologue of the o_proj GEMV that consumes o (kernels_gemv.hip, GV_ORES): no inter-workgroup
+// hand-off inside this kernel, the kernel boundary orders it.
+// Deviation from the reference (documented in DESIGN.md): the reference rounds the normalised
+// probabilities to bf16 before P.V (modeling_gemma.py:273,277); here P.V is accumulated from
+// the fp32 probabilities (closer to the fp32 result; rel. difference ~2^-9 per term).
 constexpr int DCH = 64;  // keys per chunk
 
-// scores[b][kvh][row][t] for t in this chunk; rows = the G heads (<= 16)
-__global__ void __launch_bounds__(256) k_attn_dec_scores(AttnArgs a, const StepState* st, int max_keys,
-                                                          float* __restrict__ scores) {
-    using I = HDInfo<256>;
-    const int Lk = st->kv_len + 1;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b = blockIdx.z, kvh = blockIdx.y;
-    const int t0 = blockIdx.x * DCH + wave * 16;
-    if (blockIdx.x * DCH >= Lk) return;
-    const int qi = lane & 15;
-    const bool qvalid = qi < a.G;
-    const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
-    const int key = t0 + (lane & 15);
-    const bool kvalid = key < Lk;
-    const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < I::KS; ++kk)
-        acc = mfma16(load_frag<256>(qrow, qvalid, kk, lane), load_frag<256>(krow, kvalid, kk, lane), acc);
-    float* srow = scores + ((long)(b * a.n_kv + kvh) * 16) * max_keys;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = (lane >> 4) * 4 + r;
-        if (kvalid && row < a.G) srow[(long)row * max_keys + key] = rbf(rbf(acc[r]) * a.scale);
-    }
-}
+constexpr int PSTRIDE = 16 * 256 + 32;  // per-chunk partial record: O_c[16][256], m_c[16], l_c[16]
 
-// per chunk: global softmax stats from all scores, P for the chunk, partial O = P.V (fp32)
-__global__ void __launch_bounds__(256) k_attn_dec_pv(AttnArgs a, const StepState* st, int max_keys,
-                                                      const float* __restrict__ scores, float* __restrict__ opart,
+__global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a, const StepState* st, float* __restrict__ part,
                                                       int max_chunks) {
     const int Lk = st->kv_len + 1;
+    const int nch = (Lk + DCH - 1) / DCH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.z, kvh = blockIdx.y, chunk = blockIdx.x;
+    if (chunk >= nch) return;
     const int t0 = chunk * DCH;
-    if (t0 >= Lk) return;
-    __shared__ __attribute__((aligned(16))) uint16_t P[16 * DCH];
-    __shared__ __attribute__((aligned(16))) uint16_t VT[256 * (DCH + 8)];
-    const float* sbase = scores + ((long)(b * a.n_kv + kvh) * 16) * max_keys;
-    for (int row = wave; row < 16; row += 4) {
-        if (row < a.G) {
-            const float* srow = sbase + (long)row * max_keys;
-            float m = -INFINITY;
-            for (int t = lane; t < Lk; t += 64) m = fmaxf(m, srow[t]);
-            m = wave_max(m);
-            float sum = 0.f;
-            for (int t = lane; t < Lk; t += 64) sum += expf(srow[t] - m);
-            sum = wave_sum(sum);
-            const int t = t0 + lane;
-            P[row * DCH + lane] = t < Lk ? f2bf(expf(srow[t] - m) / sum) : 0;
-        } else {
-            P[row * DCH + lane] = 0;
+    __shared__ __attribute__((aligned(16))) float S[16][DCH + 4];   // scores, then e = exp(s - m_c)
+    __shared__ __attribute__((aligned(16))) float ET[DCH][16];      // e transposed: [key][head]
+    __shared__ __attribute__((aligned(16))) float R[128][17];       // key-half reduction
+    __shared__ float stat[2][16];
+
+    // V rows of this chunk first (their latency overlaps the scores): thread = (d pair, key half),
+    // all 32 row loads in flight; rows past the cache length are clamped (their e is 0)
+    const int dp = tid & 127, kh = tid >> 7;
+    const int nk = (Lk - t0) < DCH ? (Lk - t0) : DCH;
+    uint32_t vv[DCH / 2];
+    {
+        const uint16_t* vb = a.v + b * a.v_b_stride + kvh * a.v_head_stride + 2 * dp;
+#pragma unroll
+        for (int tt = 0; tt < DCH / 2; ++tt) {
+            int t = kh * (DCH / 2) + tt;
+            t = t < nk ? t : nk - 1;
+            vv[tt] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(vb + (long)(t0 + t) * a.v_row_stride));
         }
     }
-    // V chunk [64 keys][256] -> VT[d][key]
-    const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
-    for (int e = tid; e < DCH * 32; e += 256) {
-        const int tt = e >> 5, ch = e & 31;
-        const int key = t0 + tt;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (key < Lk) v = ldg16(vbase + (long)key * a.v_row_stride + ch * 8);
-        const uint16_t* ve = reinterpret_cast<const uint16_t*>(&v);
+    float acc0[8], acc1[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) VT[(ch * 8 + j) * (DCH + 8) + tt] = ve[j];
-    }
-    __syncthreads();
-    float* ob = opart + (((long)(b * a.n_kv + kvh) * max_chunks + chunk) * 16) * 256;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int ct = wave + 4 * c;
+    for (int h = 0; h < 8; ++h) { acc0[h] = 0.f; acc1[h] = 0.f; }
+
+    // ---- scores (MFMA): wave w -> keys t0 + 16w + (lane & 15)
+    {
+        const int qi = lane & 15;
+        const bool qvalid = qi < a.G;
+        const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
+        const int key = t0 + wave * 16 + (lane & 15);
+        const bool kvalid = key < Lk;
+        const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < DCH / 32; ++ks) {
-            const short8 pa = *reinterpret_cast<const short8*>(P + (lane & 15) * DCH + ks * 32 + 8 * (lane >> 4));
-            const short8 vb =
-                *reinterpret_cast<const short8*>(VT + (ct * 16 + (lane & 15)) * (DCH + 8) + ks * 32 + 8 * (lane >> 4));
-            acc = mfma16(pa, vb, acc);
-        }
+        for (int kk = 0; kk < 8; ++kk)
+            acc = mfma16(load_frag<256>(qrow, qvalid, kk, lane), load_frag<256>(krow, kvalid, kk, lane), acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ob[((lane >> 4) * 4 + r) * 256 + ct * 16 + (lane & 15)] = acc[r];
+        for (int r = 0; r < 4; ++r)
+            S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
     }
+    __syncthreads();
+    // ---- chunk-local max / exp / sum: wave w handles rows 4w..4w+3, lane = key
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int h = wave * 4 + rr;
+        const float sv = S[h][lane];
+        const float m = wave_max(sv);
+        const float e = (t0 + lane < Lk && h < a.G) ? expf(sv - m) : 0.f;
+        ET[lane][h] = e;
+        const float l = wave_sum(e);
+        if (lane == 0) { stat[0][h] = m; stat[1][h] = l; }
+    }
+    __syncthreads();
+    // ---- O_c[h][d] = sum_t e[t][h] * v[t][d]: thread = (d pair, key half); V rows were loaded
+    // at kernel entry
+#pragma unroll
+    for (int tt = 0; tt < DCH / 2; ++tt) {
+        const int t = kh * (DCH / 2) + tt;
+        const float v0 = __uint_as_float(vv[tt] << 16), v1 = __uint_as_float(vv[tt] & 0xFFFF0000u);
+        const f32x4 e0 = *reinterpret_cast<const f32x4*>(&ET[t][0]);
+        const f32x4 e1 = *reinterpret_cast<const f32x4*>(&ET[t][4]);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            acc0[h] += e0[h] * v0; acc1[h] += e0[h] * v1;
+            acc0[h + 4] += e1[h] * v0; acc1[h + 4] += e1[h] * v1;
+        }
+    }
+    if (kh == 1) {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) { R[dp][h] = acc0[h]; R[dp][8 + h] = acc1[h]; }
+    }
+    __syncthreads();
+    float* pb = part + ((long)(b * a.n_kv + kvh) * max_chunks + chunk) * PSTRIDE;
+    if (kh == 0) {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            if (h < a.G) {
+                const float2 o = make_float2(acc0[h] + R[dp][h], acc1[h] + R[dp][8 + h]);
+                *reinterpret_cast<float2*>(pb + h * 256 + 2 * dp) = o;
+            }
+        }
+    }
+    if (tid < 32) pb[16 * 256 + tid] = stat[tid >> 4][tid & 15];
+
 }
 
-// O[b][head][d] = bf16(sum over chunks, fixed order)
-__global__ void k_attn_dec_combine(AttnArgs a, const StepState* st, const float* __restrict__ opart,
-                                   int max_chunks) {
-    const int Lk = st->kv_len + 1;
-    const int nch = (Lk + DCH - 1) / DCH;
-    const int b = blockIdx.y, kvh = blockIdx.x;
-    const float* pb = opart + ((long)(b * a.n_kv + kvh) * max_chunks) * 16 * 256;
-    for (int e = threadIdx.x; e < a.G * 256; e += blockDim.x) {
-        float s = 0.f;
-        for (int c = 0; c < nch; ++c) s += pb[(long)c * 16 * 256 + e];
-        const int row = e >> 8, d = e & 255;
-        a.o[b * a.o_b_stride + (kvh * a.G + row) * a.o_head_stride + d] = f2bf(s);
-    }
+size_t attention_decode_part_floats(int B, int n_kv, int max_chunks) {
+    return (size_t)B * n_kv * max_chunks * PSTRIDE;
 }
 
-void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int max_keys, int launch_keys,
-                      float* scores, float* opart, int max_chunks) {
+void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
+                      int max_chunks) {
     const int nch = (launch_keys + DCH - 1) / DCH;
-    dim3 grid(nch, a.n_kv, a.B);
-    hipLaunchKernelGGL(k_attn_dec_scores, grid, dim3(256), 0, s, a, st, max_keys, scores);
-    hipLaunchKernelGGL(k_attn_dec_pv, grid, dim3(256), 0, s, a, st, max_keys, scores, opart, max_chunks);
-    hipLaunchKernelGGL(k_attn_dec_combine, dim3(a.n_kv, a.B), dim3(256), 0, s, a, st, opart, max_chunks);
+    dim3 grid(nch < max_chunks ? nch : max_chunks, a.n_kv, a.B);
+    hipLaunchKernelGGL(k_attn_decode, grid, dim3(256), 0, s, a, st, part, max_chunks);
 }
 
 }  // namespace pgmi

@@ -18,7 +18,7 @@
 
 namespace pgmi {
 
-enum GemvMode : int { GV_QKV = 0, GV_RES = 1, GV_GEGLU = 2, GV_LOGITS = 3 };
+enum GemvMode : int { GV_QKV = 0, GV_RES = 1, GV_GEGLU = 2, GV_LOGITS = 3, GV_ORES = 4 };
 
 struct GemvArgs {
     const uint16_t* x;       // activation rows [nb][K] (h for the norm'd modes)
@@ -43,11 +43,19 @@ struct GemvArgs {
     uint16_t* vc;
     long kv_b_stride;
     int nkv;
+    // ORES: decode-attention partials (kernels_attn.hip) combined in the prologue
+    const float* part;
+    int max_chunks;
+    int G;
+    uint16_t* o_out;
 };
 
 // WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their
 // partial sums meet in LDS; 4/WK unit groups per workgroup.
-template <int B, int KCH, int RPW, int MODE, int WK>
+// XREG: the activation lives in registers (lane's own K chunks), the RMSNorm is computed
+// per wave (WK == 1: every wave holds the whole row), no LDS staging / barrier; used when
+// B * K/(512*WK) chunks fit in 32 VGPRs.  Otherwise the activation is staged in LDS.
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG>
 __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
     constexpr int KCW = KCH / WK;  // chunks per wave
@@ -87,8 +95,92 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     };
     if (ub < a.n_units) issue(ub);
 
-    // ---- prologue: stage (RMSNorm'd) activation rows in LDS
-    {
+    uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
+    if constexpr (MODE == GV_ORES) {
+        // (G <= 8 query heads of one KV head: PaliGemma's MQA, checked at pgmi_create)
+        // x[b][h*256 + d] = bf16(sum_c e^(m_c - M) O_c[h][d] / sum_c e^(m_c - M) l_c), chunks in
+        // a fixed order (the flash-decoding combine of k_attn_decode's partials)
+        const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
+        float* wm = reinterpret_cast<float*>(xs + B * K);  // [B][nch][8]: m_c, then weights
+        float* wl = wm + B * a.max_chunks * 8;            // [B][nch][8]: l_c
+        float* inv = wl + B * a.max_chunks * 8;           // [B][8]: sum_c w_c l_c
+        for (int i = tid; i < a.nb * nch * 8; i += 256) {
+            const int b = i / (nch * 8), c = (i / 8) % nch, h = i & 7;
+            const float* st_c = a.part + ((long)b * a.max_chunks + c) * kAttnPartStride + 16 * 256;
+            wm[(b * a.max_chunks + c) * 8 + h] = st_c[h];
+            wl[(b * a.max_chunks + c) * 8 + h] = st_c[16 + h];
+        }
+        __syncthreads();
+        if (tid < a.nb * 8) {
+            const int b = tid >> 3, h = tid & 7;
+            float M = -INFINITY;
+            for (int c = 0; c < nch; ++c) M = fmaxf(M, wm[(b * a.max_chunks + c) * 8 + h]);
+            float S = 0.f;
+            for (int c = 0; c < nch; ++c) {
+                const float w = expf(wm[(b * a.max_chunks + c) * 8 + h] - M);
+                wm[(b * a.max_chunks + c) * 8 + h] = w;
+                S += w * wl[(b * a.max_chunks + c) * 8 + h];
+            }
+            inv[b * 8 + h] = S;
+        }
+        __syncthreads();
+        for (int e8 = tid; e8 < a.nb * K / 8; e8 += 256) {
+            const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
+            const int h = e >> 8, d = e & 255;
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = 0.f;
+            const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + d;
+#pragma unroll 4
+            for (int c = 0; c < nch; ++c) {
+                const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+                const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+                const float w = wm[(b * a.max_chunks + c) * 8 + h];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
+            }
+            const float S = inv[b * 8 + h];
+            u16x8 ob;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(o[j] / S);
+            *reinterpret_cast<u16x8*>(xs + b * K + e) = ob;
+            if (a.o_out && blockIdx.x == 0) *reinterpret_cast<u16x8*>(a.o_out + (long)b * K + e) = ob;
+        }
+        for (int e8 = tid; e8 < (B - a.nb) * K / 8; e8 += 256)
+            *reinterpret_cast<uint4*>(xs + a.nb * K + e8 * 8) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+    } else if constexpr (XREG) {
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int c = 0; c < KCW; ++c)
+                xr[b][c] = (b < a.nb) ? ldg16(a.x + (long)b * K + kofs + 512 * c) : make_uint4(0, 0, 0, 0);
+        if (a.norm_w) {  // WK == 1: the wave holds the whole row
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                float ss = 0.f;
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) {
+                    const uint16_t* e = reinterpret_cast<const uint16_t*>(&xr[b][c]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { const float f = bf2f(e[j]); ss += f * f; }
+                }
+                ss = wave_sum(ss);
+                const float r = 1.0f / sqrtf(ss / (float)K + a.eps);
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) {
+                    const uint4 wv = ldg16(a.norm_w + kofs + 512 * c);
+                    const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+                    const uint16_t* e = reinterpret_cast<const uint16_t*>(&xr[b][c]);
+                    u16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r) * (1.0f + bf2f(we[j])));
+                    xr[b][c] = *reinterpret_cast<const uint4*>(&o);
+                }
+            }
+        }
+    } else {
+        // ---- prologue: stage (RMSNorm'd) activation rows in LDS
         float ss[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) ss[b] = 0.f;
@@ -156,7 +248,9 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
         for (int c = 0; c < KCW; ++c) {
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-                const uint4 xv = *reinterpret_cast<const uint4*>(xs + b * K + kofs + 512 * c);
+                uint4 xv;
+                if constexpr (XREG) xv = xr[b][c];
+                else xv = *reinterpret_cast<const uint4*>(xs + b * K + kofs + 512 * c);
 #pragma unroll
                 for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -207,7 +301,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 if (b >= a.nb) break;
-                if constexpr (MODE == GV_RES) {
+                if constexpr (MODE == GV_RES || MODE == GV_ORES) {
                     if (lane == 0) {
                         uint16_t* hp = a.out + (long)b * a.n_units + u;
                         *hp = f2bf(rbf(acc[i][0][b]) + bf2f(*hp));
@@ -277,17 +371,19 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
 
 template <int B, int KCH, int RPW, int MODE, int WK = 1>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
-    const size_t lds = (size_t)B * KCH * 512 * sizeof(uint16_t);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK>),
+    constexpr bool XREG = (MODE != GV_ORES) && B * (KCH / WK) <= 8;
+    size_t lds = XREG ? 0 : (size_t)B * KCH * 512 * sizeof(uint16_t);
+    if (MODE == GV_ORES) lds += ((size_t)B * a.max_chunks * 16 + B * 8) * sizeof(float);
+    static size_t attr = 0;  // largest dynamic LDS size granted so far
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        attr = lds;
     }
     constexpr int per_block = (4 / WK) * RPW;
     int blocks = (a.n_units + per_block - 1) / per_block;
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK, XREG>), dim3(blocks), dim3(256), lds, s, a);
 }
 
 // K = 2048 (hidden); nh q heads, nkv kv heads of 256
@@ -318,18 +414,30 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
             const int nb = (B - b0) < 4 ? (B - b0) : 4;
             GemvArgs c = a;
             c.x = x + (long)b0 * K; c.out = h_inout + (long)b0 * N; c.nb = nb;
-            if (nb <= 1) launch_gemv<1, 32, 2, GV_RES, 4>(s, c);
+            if (nb <= 1) launch_gemv<1, 32, 2, GV_RES, 4>(s, c, 512);
             else if (nb <= 2) launch_gemv<2, 32, 2, GV_RES, 4>(s, c);
             else launch_gemv<4, 32, 2, GV_RES, 4>(s, c);
         }
     }
 }
 
+void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out) {
+    GemvArgs a{};
+    a.x = nullptr; a.norm_w = nullptr; a.W = Wo; a.n_units = N; a.K = G * 256; a.nb = B; a.out = h_inout;
+    a.part = part; a.max_chunks = max_chunks; a.G = G; a.st = st; a.o_out = o_out;
+    // grid capped so each workgroup's combine prologue is amortised over 8 output rows
+    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, 256);
+    else if (B <= 2) launch_gemv<2, 4, 2, GV_ORES>(s, a, 256);
+    else if (B <= 4) launch_gemv<4, 4, 1, GV_ORES>(s, a, 256);
+    else launch_gemv<8, 4, 1, GV_ORES>(s, a, 256);
+}
+
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* Wgu,
                 int I, uint16_t* act) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
-    if (B <= 1) L_(1, 4, 2, GV_GEGLU);
+    if (B <= 1) launch_gemv<1, 4, 2, GV_GEGLU>(s, a, 1024);
     else if (B <= 2) L_(2, 4, 2, GV_GEGLU);
     else if (B <= 4) L_(4, 4, 2, GV_GEGLU);
     else L_(8, 4, 1, GV_GEGLU);

@@ -45,6 +45,10 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
               uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride);
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout);
+// o_proj + residual whose input is the combine of the decode-attention partials (MQA:
+// n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output
+void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out);
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                 const uint16_t* Wgu, int I, uint16_t* act);
 int gemv_logits_blocks();
@@ -68,9 +72,13 @@ struct AttnArgs {
 };
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
 // decode: Lq == 1, rows = the G heads; keys split over chunks; kv length from StepState (+1)
-// max_keys = allocated key stride of `scores`; launch_keys = upper bound on kv_len+1 this call
-void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int max_keys, int launch_keys,
-                      float* scores, float* opart, int max_chunks);
+// flash-decoding over 64-key chunks (partials only; the combine is gemv_o_attn's prologue);
+// launch_keys = upper bound on kv_len+1 this call
+void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
+                      int max_chunks);
+constexpr int kAttnChunk = 64;
+constexpr int kAttnPartStride = 16 * 256 + 32;  // floats per (b, kv head, chunk) record
+size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
 
 // ---------------------------------------------------------------- misc

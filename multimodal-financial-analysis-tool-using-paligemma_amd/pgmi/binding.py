@@ -1,0 +1,107 @@
+"""Binds the drop-in nn.Module trees (modeling_gemma / modeling_siglip) to an Engine.
+
+On the first forward on a GPU the module's parameters are copied into the engine's bf16
+weight slab; bf16 parameters are then re-pointed at their slab views, so the model holds one
+copy of the weights and later in-place updates (load_state_dict) land in the slab.  A cheap
+fingerprint (storage pointers and version counters of a parameter sample) detects
+.to(...)/re-assignment and rebuilds the engine.
+"""
+from __future__ import annotations
+
+import weakref
+
+import torch
+
+from .engine import Engine
+
+# capacities of engines built by the Python API (pgmi_config.max_batch / max_seq / max_kv)
+DEFAULT_MAX_BATCH = 8
+DEFAULT_MAX_SEQ = 1472
+
+_DUMMY_TEXT = {"vocab_size": 8, "hidden_size": 2048, "intermediate_size": 16384, "num_hidden_layers": 0,
+               "num_attention_heads": 8, "num_key_value_heads": 1, "head_dim": 256,
+               "max_position_embeddings": 64, "rms_norm_eps": 1e-6, "rope_theta": 10000.0}
+_DUMMY_VISION = {"hidden_size": 1152, "intermediate_size": 4304, "num_hidden_layers": 0,
+                 "num_attention_heads": 16, "num_channels": 3, "image_size": 14, "patch_size": 14,
+                 "layer_norm_eps": 1e-6}
+
+
+def _device_of(module) -> torch.device:
+    p = next(module.parameters(), None)
+    if p is None or p.device.type != "cuda":
+        raise RuntimeError(
+            "libpgmi runs the PaliGemma path on an MI355X GPU only (no CPU fallback): move the model to the "
+            "GPU with .to('cuda') first")
+    return p.device
+
+
+def _fingerprint(module):
+    ps = list(module.parameters())
+    sample = ps[:: max(1, len(ps) // 16)] + ps[-1:]
+    return tuple((p.data_ptr(), p._version, p.dtype) for p in sample)
+
+
+class _Bound:
+    def __init__(self, engine, fp):
+        self.engine, self.fp = engine, fp
+
+
+def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
+    """Engine for `module` (parameters named prefix + local name in the slab)."""
+    dev = _device_of(module)
+    b = module.__dict__.get("_pgmi_bound")
+    if b is not None and b.fp == _fingerprint(module) and b.engine.device == dev:
+        return b.engine
+    eng = Engine(cfg, device=dev, max_batch=DEFAULT_MAX_BATCH, max_seq=DEFAULT_MAX_SEQ)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            full = prefix + name
+            view = eng.views.get(full)
+            if view is None:
+                continue  # e.g. the tied lm_head (modeling_gemma.py:396-397)
+            if tuple(p.shape) != tuple(view.shape):
+                raise ValueError(f"{full}: shape {tuple(p.shape)} != {tuple(view.shape)}")
+            view.copy_(p.detach())
+            if p.dtype == torch.bfloat16 and p.device == dev:
+                p.data = view
+    eng.prepare(inv_freq=inv_freq)
+    module.__dict__["_pgmi_bound"] = _Bound(eng, _fingerprint(module))
+    return eng
+
+
+def set_owner(child, owner):
+    """Let a submodule (vision tower, language model) run on its parent's engine."""
+    child.__dict__["_pgmi_owner"] = weakref.ref(owner)
+
+
+def owner_of(child):
+    r = child.__dict__.get("_pgmi_owner")
+    return r() if r is not None else None
+
+
+def vision_cfg(vc) -> dict:
+    v = {k: getattr(vc, k) for k in ("hidden_size", "intermediate_size", "num_hidden_layers", "num_attention_heads",
+                                     "num_channels", "image_size", "patch_size", "layer_norm_eps")}
+    return {"vision_config": v, "text_config": dict(_DUMMY_TEXT), "image_token_index": 7, "projection_dim": 2048,
+            "pad_token_id": None}
+
+
+def text_cfg(tc) -> dict:
+    t = {k: getattr(tc, k) for k in ("vocab_size", "hidden_size", "intermediate_size", "num_hidden_layers",
+                                     "num_attention_heads", "num_key_value_heads", "head_dim",
+                                     "max_position_embeddings", "rms_norm_eps", "rope_theta")}
+    return {"vision_config": dict(_DUMMY_VISION), "text_config": t, "image_token_index": -7,
+            "projection_dim": 2048, "pad_token_id": getattr(tc, "pad_token_id", None)}
+
+
+def vision_forward(transformer, pixel_values, prefix="vision_tower.vision_model."):
+    """SiglipVisionTransformer.forward (modeling_siglip.py:236-244) through pgmi_vision."""
+    owner = owner_of(transformer)
+    if owner is not None:
+        eng = owner._pgmi_engine()
+    else:
+        eng = bind(transformer, vision_cfg(transformer.config), prefix)
+    px = pixel_values
+    if px.dtype not in (torch.float32, torch.bfloat16):
+        px = px.float()
+    return eng.vision(px)

@@ -133,6 +133,25 @@ class Engine:
         return torch.empty((t["t_layers"], 2, batch, T, t["t_kv_heads"] * t["t_head_dim"]),
                            dtype=torch.bfloat16, device=self.device)
 
+    def scratch_kv(self, batch: int, tokens: int) -> torch.Tensor:
+        """Cache for calls without a KVCache (kv_cache=None: the no-KV ablation mode)."""
+        cur = getattr(self, "_scratch_kv", None)
+        if cur is None or cur.shape[2] < batch or cur.shape[3] < tokens:
+            cur = self.new_kv(max(batch, cur.shape[2] if cur is not None else 0),
+                              max(tokens, cur.shape[3] if cur is not None else 0))
+            self._scratch_kv = cur
+        if cur.shape[2] != batch:
+            return self.new_kv(batch, tokens)
+        return cur
+
+    def logits_buffer(self, batch: int) -> torch.Tensor:
+        """Persistent decode logits buffer (a stable pointer lets the decode hipGraph be reused)."""
+        buf = self._logits_buf.get(batch)
+        if buf is None:
+            buf = torch.empty((batch, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+            self._logits_buf[batch] = buf
+        return buf
+
     # ------------------------------------------------------------------ forward pieces
     def _s(self):
         return N.stream_handle(self.device)

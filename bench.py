@@ -99,6 +99,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from pgmi import Engine
+    from pgmi.dist import broadcast_slab
     from pgmi.synthetic import init_policy, paligemma_3b_config, prompt_ids
 
     cfg = paligemma_3b_config(a.image_size)
@@ -116,7 +117,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        dist.broadcast(eng.slab, src=0)
+        broadcast_slab(eng.slab, src=0)
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - t0) * 1e3
     eng.prepare()

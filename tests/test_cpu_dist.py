@@ -1,0 +1,50 @@
+"""N > 1 path on CPU with gloo, world_size 2: weight broadcast from rank 0, image sharding,
+token gather (the only collectives of the multi-GPU replicas design, pgmi/dist.py)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path.insert(0, os.path.join(repo, "multimodal-financial-analysis-tool-using-paligemma_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pgmi.dist import broadcast_slab, gather_tokens, shard_range
+    slab = torch.arange(1000, dtype=torch.uint8) if rank == 0 else torch.zeros(1000, dtype=torch.uint8)
+    broadcast_slab(slab, src=0)
+    lo, hi = shard_range(64, rank, world)
+    toks = torch.arange(lo, hi).reshape(-1, 1).repeat(1, 3)
+    allt = gather_tokens(toks)
+    q.put((rank, bool(torch.equal(slab, torch.arange(1000, dtype=torch.uint8))), allt[:, 0].tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, ids in res:
+        assert ok
+        assert ids == list(range(64))

@@ -1,0 +1,164 @@
+"""Host-side logic and the C ABI surface, CPU only (no compute calls without a GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from tests_helpers import pixels_from_u8
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "pgmi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pgmi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pgmi import _native as N
+    lib = N.lib()
+    declared = header_functions()
+    assert len(declared) >= 25
+    for name in declared:
+        assert hasattr(lib, name), name
+    # the ctypes binding covers the whole header
+    assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
+    assert lib.pgmi_version().startswith(b"pgmi")
+
+
+def test_create_validates_config_without_gpu():
+    """pgmi_create only builds the weight layout (no device memory): it runs here."""
+    from pgmi import _native as N
+    from pgmi.engine import config_dict
+    from pgmi.synthetic import paligemma_3b_config
+    lib = N.lib()
+    cd = config_dict(paligemma_3b_config())
+    c = N.PgmiConfig()
+    for k, _ in N.PgmiConfig._fields_:
+        if k not in ("max_batch", "max_seq", "max_kv"):
+            setattr(c, k, cd[k])
+    c.max_batch, c.max_seq, c.max_kv = 1, 288, 1024
+    h = ctypes.c_void_p()
+    assert lib.pgmi_create(0, ctypes.byref(c), ctypes.byref(h)) == 0
+    # slab: every reference parameter of PaliGemma-3B (lm_head tied), 256-B aligned, 2,923,466,480 params
+    n = lib.pgmi_weight_count(h)
+    total = 0
+    for i in range(n):
+        name, off, shape, nd = ctypes.c_char_p(), ctypes.c_int64(), (ctypes.c_int64 * 4)(), ctypes.c_int()
+        assert lib.pgmi_weight_info(h, i, ctypes.byref(name), ctypes.byref(off), ctypes.byref(shape), ctypes.byref(nd)) == 0
+        assert off.value % 256 == 0
+        total += int(np.prod([shape[j] for j in range(nd.value)]))
+    assert total == 2_923_466_480  # SURVEY.md sec.3.5 (the tied lm_head counted once)
+    assert lib.pgmi_weights_bytes(h) >= 2 * total
+    assert lib.pgmi_kv_bytes(h, 1, 1024) == 18 * 2 * 1024 * 256 * 2
+    lib.pgmi_destroy(h)
+    # invalid configs are rejected with PGMI_E_ARG and a message
+    c.t_kv_heads = 2
+    assert lib.pgmi_create(0, ctypes.byref(c), ctypes.byref(h)) == N.PGMI_E_ARG
+    assert b"MQA" in lib.pgmi_last_error()
+
+
+def test_fused_layout_adjacency():
+    """q|k|v (and gate|up) are adjacent in the slab so one GEMM/GEMV covers them."""
+    from pgmi import _native as N
+    from pgmi.engine import config_dict
+    from pgmi.synthetic import paligemma_3b_config
+    lib = N.lib()
+    cd = config_dict(paligemma_3b_config())
+    c = N.PgmiConfig()
+    for k, _ in N.PgmiConfig._fields_:
+        if k not in ("max_batch", "max_seq", "max_kv"):
+            setattr(c, k, cd[k])
+    c.max_batch, c.max_seq, c.max_kv = 1, 288, 1024
+    h = ctypes.c_void_p()
+    assert lib.pgmi_create(0, ctypes.byref(c), ctypes.byref(h)) == 0
+    info = {}
+    for i in range(lib.pgmi_weight_count(h)):
+        name, off, shape, nd = ctypes.c_char_p(), ctypes.c_int64(), (ctypes.c_int64 * 4)(), ctypes.c_int()
+        lib.pgmi_weight_info(h, i, ctypes.byref(name), ctypes.byref(off), ctypes.byref(shape), ctypes.byref(nd))
+        info[name.value.decode()] = (off.value, int(np.prod([shape[j] for j in range(nd.value)])) * 2)
+    lib.pgmi_destroy(h)
+    for p in ("language_model.model.layers.5.self_attn.", "vision_tower.vision_model.encoder.layers.3.self_attn."):
+        q, k, v = (info[p + f"{n}_proj.weight"] for n in "qkv")
+        assert q[0] + q[1] == k[0] and k[0] + k[1] == v[0]
+    g, u = info["language_model.model.layers.7.mlp.gate_proj.weight"], info["language_model.model.layers.7.mlp.up_proj.weight"]
+    assert g[0] + g[1] == u[0]
+
+
+def test_synthetic_policy_matches_oracle():
+    from oracle import weights as OW
+    from pgmi import synthetic as S
+    for image in (224, 448):
+        cfg = OW.full_config(image)
+        for name, shape in OW.param_shapes(cfg).items():
+            assert S.init_policy(name, shape) == OW.init_policy(name, shape), name
+    assert S.paligemma_3b_config(448) == OW.full_config(448)
+    ids = S.prompt_ids(257152, 256, 257216)
+    assert ids.shape == (1, 288) and ids[0, 256] == 2 and ids[0, -1] == 108
+
+
+def test_kvcache_reference_semantics():
+    """KVCache driven through update() behaves as modeling_gemma.py:10-36."""
+    import modeling_gemma as MG
+    kv = MG.KVCache()
+    assert kv.num_items() == 0
+    k = torch.randn(1, 1, 5, 256)
+    kv.update(k, k, 0)
+    kv.update(k, k, 1)
+    kk, vv = kv.update(torch.randn(1, 1, 1, 256), torch.randn(1, 1, 1, 256), 0)
+    assert kk.shape == (1, 1, 6, 256) and kv.num_items() == 6
+    assert len(kv.key_cache) == 2
+
+
+def test_positions_helper():
+    import modeling_gemma as MG
+    p = MG._positions_2d(torch.tensor([[289.0]]), 1, 1)
+    assert p.dtype == torch.int64 and p.tolist() == [[289]]
+    p = MG._positions_2d(torch.arange(5), 2, 5)
+    assert p.shape == (2, 5) and p[1].tolist() == [0, 1, 2, 3, 4]
+    p = MG._positions_2d(torch.tensor([[7.0], [7.0]]), 2, 3)  # patched merge, q_len > 1
+    assert p.tolist() == [[7, 7, 7], [7, 7, 7]]
+
+
+def test_configs_and_module_tree():
+    import modeling_gemma as MG
+    from pgmi.synthetic import paligemma_3b_config
+    cfg = MG.PaliGemmaConfig(**{k: v for k, v in paligemma_3b_config().items() if k not in ("bos_token_id", "eos_token_id")})
+    assert cfg.vision_config.num_image_tokens is None and cfg.text_config.num_image_tokens == 256
+    assert cfg.vision_config.projection_dim == 2048 and cfg.vocab_size == 257216
+    with torch.device("meta"):
+        m = MG.PaliGemmaForConditionalGeneration(cfg)
+    m.tie_weights()
+    n = sum(p.numel() for p in m.parameters())
+    assert n == 2_923_466_480
+    # no CPU fallback: a model that is not on the GPU refuses to run
+    with pytest.raises(RuntimeError):
+        m(input_ids=torch.zeros(1, 4, dtype=torch.long), attention_mask=torch.ones(1, 4, dtype=torch.long))
+
+
+def test_processing_matches_reference_arithmetic(golden_dir):
+    import processing_paligemma as P
+    d = np.load(os.path.join(golden_dir, "pixels.npz"))
+    u8 = d["u8_1_224"]
+    ours = P.normalize(P.rescale(u8, 1 / 255.0), P.IMAGENET_STANDARD_MEAN, P.IMAGENET_STANDARD_STD).transpose(2, 0, 1)
+    assert np.array_equal(ours, pixels_from_u8(u8))
+    from PIL import Image
+    img = Image.fromarray(d["u8_0_448"])
+    out = P.process_images([img], size=(224, 224), resample=Image.Resampling.BICUBIC, rescale_factor=1 / 255.0,
+                           image_mean=P.IMAGENET_STANDARD_MEAN, image_std=P.IMAGENET_STANDARD_STD)
+    assert out[0].shape == (3, 224, 224) and out[0].dtype == np.float32
+    assert P.add_image_tokens_to_prompt("hi", "<bos>", 3, "<image>") == "<image><image><image><bos>hi\n"
+
+
+def test_shard_range():
+    from pgmi.dist import shard_range
+    for n in (1, 7, 64):
+        for w in (1, 2, 3, 8):
+            got = [shard_range(n, r, w) for r in range(w)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(got[i][1] == got[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in got) - min(h - l for l, h in got) <= 1

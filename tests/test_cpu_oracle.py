@@ -1,0 +1,151 @@
+"""The oracle (oracle/paligemma_np.py, numpy restatement of the reference) pinned against the
+golden vectors the reference modules produced (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import paligemma_np as O
+from oracle import weights as W
+
+SEED = 1234
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def gold(golden_dir):
+    return np.load(os.path.join(golden_dir, "small_bf16.npz"))
+
+
+@pytest.fixture(scope="module")
+def small():
+    cfg = W.small_config()
+    return cfg, W.synthetic_state_dict_f32(cfg, SEED)
+
+
+@pytest.fixture(scope="module")
+def prefill(small, gold):
+    cfg, P = small
+    taps = {}
+    lg, kv = O.paligemma_prefill(P, cfg, gold["ids"], O.from_bits(gold["pixels_bits"]), taps=taps)
+    return lg, kv, taps
+
+
+def test_bf16_rounding_is_rne():
+    x = np.array([1.0, 1.00390625, 1.005859375, -2.5e-3, 3.0e38], np.float32)
+    b = O.bf16(x)
+    assert b[0] == 1.0 and b[1] == 1.0 and b[2] == np.float32(1.0078125)
+    assert np.array_equal(O.from_bits(O.bf16_bits(x)), b)
+
+
+def test_vision_embeddings_exact(prefill, gold):
+    """patch conv + bias + position embedding: bit-exact vs the reference."""
+    _, _, taps = prefill
+    assert np.array_equal(taps["vision_embeddings"][:, ::8], O.from_bits(gold["tap_vision_embeddings"]))
+
+
+@pytest.mark.parametrize("name,tol", [("vision_layer0", 6e-3), ("vision_layer1", 1e-2), ("image_features", 1e-2),
+                                      ("text_layer0", 3e-2), ("text_layer1", 4e-2)])
+def test_layer_outputs(prefill, gold, name, tol):
+    _, _, taps = prefill
+    assert rel(taps[name][:, ::8], O.from_bits(gold["tap_" + name])) < tol
+
+
+def test_per_op_teacher_forced(small, gold):
+    """Each op restated on the reference's own inputs (taps) reproduces the reference's output."""
+    cfg, P = small
+    g = lambda k: O.from_bits(gold["tap_" + k])  # noqa: E731
+    # text layer 0 input norm -> q projection (rows ::8 of the taps)
+    x = g("t0_ln_in")
+    q = O.linear(x, P["language_model.model.layers.0.self_attn.q_proj.weight"])
+    assert rel(q, g("t0_q")) < 1e-3
+    # vision layer 0: LN1 -> q
+    qv = O.linear(g("v0_ln1"), P["vision_tower.vision_model.encoder.layers.0.self_attn.q_proj.weight"],
+                  P["vision_tower.vision_model.encoder.layers.0.self_attn.q_proj.bias"])
+    assert rel(qv, g("v0_q")) < 1e-3
+
+
+def test_merge_exact(gold):
+    """_merge_input_ids_with_image_features (modeling_gemma.py:468-537) restated: text rows and
+    scaled image rows are bit-exact vs the embeddings the reference fed its language model."""
+    cfg = W.small_config()
+    P = {"language_model.model.embed_tokens.weight": _embed(cfg)}
+    feats_rows = O.from_bits(gold["tap_image_features"])  # rows 0, 8, 16, ... of the image features
+    ref = O.from_bits(gold["tap_merged_embeds"])           # rows 0, 8, 16, ... of the merged embeds
+    m = O.merge(P, cfg, None, gold["ids"])                  # text rows (image rows left zero)
+    text_rows = np.arange(0, gold["ids"].shape[1], 8) >= 256
+    assert np.array_equal(m[:, ::8][:, text_rows], ref[:, text_rows])
+    scaled = O.bf16(feats_rows / np.float32(cfg["hidden_size"] ** 0.5))
+    assert np.array_equal(scaled[:, : int((~text_rows).sum())], ref[:, ~text_rows])
+
+
+_EMB = {}
+
+
+def _embed(cfg):
+    if "e" not in _EMB:
+        _EMB["e"] = W.gen_f32("language_model.model.embed_tokens.weight", W.param_shapes(cfg)[
+            "language_model.model.embed_tokens.weight"], SEED)
+    return _EMB["e"]
+
+
+def test_prefill_logits(prefill, gold):
+    lg, _, _ = prefill
+    assert rel(lg[:, -1], gold["prefill_logits_last"]) < 3e-2
+    assert rel(lg[:, ::32], O.from_bits(gold["prefill_logits_rows"])) < 3e-2
+
+
+def test_kv_cache_rows(prefill, gold):
+    _, kv, _ = prefill
+    assert rel(kv.k[0][:, :, ::4], O.from_bits(gold["k0"])) < 1e-2
+    assert rel(kv.v[-1][:, :, ::4], O.from_bits(gold["v_last"])) < 3e-2
+
+
+def test_greedy_tokens(small, gold):
+    """inference.py semantics (position gap L+1): tokens equal the reference's wherever the
+    reference's top-2 margin exceeds 0.25."""
+    cfg, P = small
+    toks, _ = O.greedy_generate(P, cfg, gold["ids"], O.from_bits(gold["pixels_bits"]), 16)
+    ref = gold["greedy_tokens"]
+    s = np.sort(O.from_bits(gold["greedy_logits"]), -1)
+    margin = s[:, -1] - s[:, -2]
+    diff = np.nonzero(toks[0] != ref)[0]
+    assert len(diff) == 0 or margin[diff[0]] < 0.25
+
+
+def test_rope_tables():
+    """inv_freq / cos / sin as GemmaRotaryEmbedding computes them (modeling_gemma.py:151,178-185)."""
+    import torch
+    inv_t = 1.0 / (10000.0 ** (torch.arange(0, 256, 2, dtype=torch.int64).float() / 256))
+    inv = O.inv_freq()
+    assert np.max(np.abs(inv - inv_t.numpy()) / inv_t.numpy()) < 2e-7
+    pos = np.array([[0, 1, 287, 289, 8191]])
+    c, s = O.rope_cos_sin(pos, inv_t.numpy())
+    f = (inv_t[None, :, None] @ torch.tensor(pos, dtype=torch.float32)[:, None, :]).transpose(1, 2)
+    emb = torch.cat((f, f), -1)
+    ct, st = emb.cos().to(torch.bfloat16).float().numpy(), emb.sin().to(torch.bfloat16).float().numpy()
+    assert (c != ct).mean() < 1e-3 and (s != st).mean() < 1e-3
+
+
+def test_pixels_from_u8(golden_dir):
+    """process_images restated on the stored BICUBIC output equals the reference's fp32 pixels
+    (sums recorded by make_golden.py)."""
+    d = np.load(os.path.join(golden_dir, "pixels.npz"))
+    from tests_helpers import pixels_from_u8
+    keys = sorted(k.replace("u8_", "px_") for k in d.files if k.startswith("u8_"))
+    sums = [pixels_from_u8(d[k.replace("px_", "u8_")]).astype(np.float64).sum() for k in keys]
+    assert np.allclose(sums, d["px_sum"], rtol=0, atol=1e-6)
+
+
+def test_full_size_fixture_consistency(golden_dir):
+    """The full-shape fixtures are self-consistent: reference bf16 vs fp32 error is small (the
+    synthetic init is well conditioned) and the stored top-k agree with the stored tokens."""
+    b = np.load(os.path.join(golden_dir, "full_bf16.npz"))
+    f = np.load(os.path.join(golden_dir, "full_fp32.npz"))
+    assert b["tokens"].shape[-1] == 64
+    assert np.array_equal(b["topk_idx"][:, 0], b["tokens"].reshape(-1))
+    assert float(f["ref_bf16_rel_l2"].max()) < 0.05

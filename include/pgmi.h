@@ -125,6 +125,11 @@ int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* ou
  * 4 final norm + lm_head (+argmax partials; layer ignored). */
 int pgmi_decode_kernel(pgmi_ctx* ctx, int which, int layer, int B, void* stream);
 
+/* Tuning hook: force the prefill GEMM tile configuration (0: 288x64, 1: 288x32, 2: 256x64,
+ * 3: 256x32, 4: 128x128, 5: 128x64) and split-K factor for subsequent calls; cfg < 0 restores
+ * the automatic plan. */
+int pgmi_tune_gemm(int cfg, int split);
+
 /* ---- single-op entry points (kernel-level parity tests) ---------------------------------- */
 /* out = epilogue(A[M,K] . W[N,K]^T): epi 0 store, 1 +bias, 2 +bias,gelu, 3 +bias,+res, 4 +res,
  * 6 fp32 out (out is float*), 7 GeGLU with up rows at W + N*K */

@@ -461,8 +461,10 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
     e.ldo = D;
     gemm(s, x->vP, x->kpad, x->patch_w, x->kpad, rows, D, x->kpad, EPI_BIAS_POS, e, x->ws, x->ws_bytes);
     const float scale = (float)std::pow((double)(D / c.v_heads), -0.5);  // head_dim**-0.5 (:89)
+    // LayerNorm1 of layer 0; every later LayerNorm is fused with the preceding projection's
+    // split-K reduction + bias + residual (splitk_res_norm)
+    layernorm(s, x->vX, VL(x, 0, "layer_norm1.weight"), VL(x, 0, "layer_norm1.bias"), eps, x->vT, rows, D);
     for (int i = 0; i < c.v_layers; ++i) {
-        layernorm(s, x->vX, VL(x, i, "layer_norm1.weight"), VL(x, i, "layer_norm1.bias"), eps, x->vT, rows, D);
         EpiArgs q{};
         q.bias = VL(x, i, "self_attn.q_proj.bias");  // q|k|v biases adjacent
         q.out = x->vQKV;
@@ -478,17 +480,26 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
         EpiArgs o{};
         o.bias = VL(x, i, "self_attn.out_proj.bias");
         o.res = x->vX; o.ldr = D; o.out = x->vX; o.ldo = D;
-        gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws, x->ws_bytes);
-        layernorm(s, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"), eps, x->vT, rows, D);
+        int sp = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
+                      x->ws_bytes, 0, true);
+        splitk_res_norm(s, x->ws, sp, o.bias, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"), eps,
+                        x->vT, rows, D);
         EpiArgs f1{};
         f1.bias = VL(x, i, "mlp.fc1.bias"); f1.out = x->vH; f1.ldo = Iv;
         gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
         EpiArgs f2{};
         f2.bias = VL(x, i, "mlp.fc2.bias"); f2.res = x->vX; f2.ldr = D; f2.out = x->vX; f2.ldo = D;
-        gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws, x->ws_bytes);
+        sp = gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws, x->ws_bytes, 0,
+                  true);
+        const bool last = i + 1 == c.v_layers;
+        splitk_res_norm(s, x->ws, sp, f2.bias, x->vX,
+                        last ? W(x, "vision_tower.vision_model.post_layernorm.weight") : VL(x, i + 1, "layer_norm1.weight"),
+                        last ? W(x, "vision_tower.vision_model.post_layernorm.bias") : VL(x, i + 1, "layer_norm1.bias"),
+                        eps, last ? reinterpret_cast<uint16_t*>(feats) : x->vT, rows, D);
     }
-    layernorm(s, x->vX, W(x, "vision_tower.vision_model.post_layernorm.weight"),
-              W(x, "vision_tower.vision_model.post_layernorm.bias"), eps, reinterpret_cast<uint16_t*>(feats), rows, D);
+    if (c.v_layers == 0)
+        layernorm(s, x->vX, W(x, "vision_tower.vision_model.post_layernorm.weight"),
+                  W(x, "vision_tower.vision_model.post_layernorm.bias"), eps, reinterpret_cast<uint16_t*>(feats), rows, D);
     LAUNCHCHK();
     return 0;
 }
@@ -547,14 +558,19 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
     }
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
+    const uint16_t* fnorm = W(x, "language_model.model.norm.weight");
+    // input RMSNorm of layer 0; every later RMSNorm (and the final norm) is fused with the
+    // preceding projection's split-K reduction + residual (splitk_res_norm)
+    rmsnorm(s, x->Hs, c.t_layers ? TL(x, 0, "input_layernorm.weight") : fnorm, eps, x->Tn, R, H);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-        rmsnorm(s, x->Hs, TL(x, i, "input_layernorm.weight"), eps, x->Tn, R, H);
         EpiArgs q{};
         q.out = x->QKV; q.ldo = QKVN;
-        gemm(s, x->Tn, H, TL(x, i, "self_attn.q_proj.weight"), H, R, QKVN, H, EPI_STORE, q, x->ws, x->ws_bytes);
-        rope_kv_append(s, x->QKV, B, L, NH, NKV, x->dpos, x->cosT, x->sinT, c.t_max_pos, x->Qr, Kc, Vc, kvb, kv_start);
+        int sp = gemm(s, x->Tn, H, TL(x, i, "self_attn.q_proj.weight"), H, R, QKVN, H, EPI_STORE, q, x->ws,
+                      x->ws_bytes, 0, true);
+        rope_kv_append(s, x->QKV, x->ws, sp, B, L, NH, NKV, x->dpos, x->cosT, x->sinT, c.t_max_pos, x->Qr, Kc, Vc, kvb,
+                       kv_start);
         AttnArgs a{};
         a.q = x->Qr; a.q_b_stride = (long)L * NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -565,21 +581,24 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
         attention_prefill(s, 256, a);
         EpiArgs o{};
         o.res = x->Hs; o.ldr = H; o.out = x->Hs; o.ldo = H;
-        gemm(s, x->AO, H, TL(x, i, "self_attn.o_proj.weight"), H, R, H, NH * HD, EPI_RES, o, x->ws, x->ws_bytes);
-        rmsnorm(s, x->Hs, TL(x, i, "post_attention_layernorm.weight"), eps, x->Tn, R, H);
+        sp = gemm(s, x->AO, H, TL(x, i, "self_attn.o_proj.weight"), H, R, H, NH * HD, EPI_RES, o, x->ws, x->ws_bytes,
+                  0, true);
+        splitk_res_norm(s, x->ws, sp, nullptr, x->Hs, TL(x, i, "post_attention_layernorm.weight"), nullptr, eps, x->Tn,
+                        R, H);
         EpiArgs g{};
         g.out = x->ACT; g.ldo = c.t_intermediate;
         gemm(s, x->Tn, H, TL(x, i, "mlp.gate_proj.weight"), H, R, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
              x->ws_bytes, c.t_intermediate);
         EpiArgs d{};
         d.res = x->Hs; d.ldr = H; d.out = x->Hs; d.ldo = H;
-        gemm(s, x->ACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, R, H,
-             c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes);
+        sp = gemm(s, x->ACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, R, H,
+                  c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes, 0, true);
+        const bool last = i + 1 == c.t_layers;
+        splitk_res_norm(s, x->ws, sp, nullptr, x->Hs, last ? fnorm : TL(x, i + 1, "input_layernorm.weight"), nullptr,
+                        eps, x->Tn, R, H);
     }
-    const uint16_t* fnorm = W(x, "language_model.model.norm.weight");
     if (logits_rows == 0) {
-        rmsnorm(s, x->Hs, fnorm, eps, x->Tn, R, H);
-        EpiArgs l{};
+        EpiArgs l{};  // Tn holds the final RMSNorm (modeling_gemma.py:379)
         l.out_f32 = logits; l.ldo = c.t_vocab;
         gemm(s, x->Tn, H, E, H, R, c.t_vocab, H, EPI_F32, l, x->ws, x->ws_bytes);
     } else {
@@ -697,6 +716,12 @@ int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
         default: return fail(PGMI_E_ARG, "unknown kernel id");
     }
     LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_tune_gemm(int cfg, int split) {
+    if (cfg > 5 || split < 0 || split > 16) return fail(PGMI_E_ARG, "bad GEMM plan");
+    gemm_force_plan(cfg, split);
     return 0;
 }
 

@@ -225,7 +225,9 @@ void scale_rows(hipStream_t s, const uint16_t* x, long n, float a, uint16_t* out
 // ---------------------------------------------------------------- RoPE + KV append (prefill)
 // qkv rows: [q (nh*256) | k (nkv*256) | v (nkv*256)].  apply_rotary_pos_emb rounds three
 // times (q*cos, rotate_half(q)*sin, sum), modeling_gemma.py:197-198.
-__global__ void k_rope_kv(const uint16_t* __restrict__ qkv, int L, int nh, int nkv, const int64_t* __restrict__ pos,
+template <bool PART>
+__global__ void k_rope_kv(const uint16_t* __restrict__ qkv, const float* __restrict__ ws, int split, long slab,
+                          int L, int nh, int nkv, const int64_t* __restrict__ pos,
                           const uint16_t* __restrict__ cosT, const uint16_t* __restrict__ sinT, int max_pos,
                           uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
                           long kv_b_stride, int kv_start) {
@@ -235,11 +237,19 @@ __global__ void k_rope_kv(const uint16_t* __restrict__ qkv, int L, int nh, int n
     if (p < 0) p = 0;
     if (p > max_pos - 1) p = max_pos - 1;
     const int ncol = (nh + 2 * nkv) * 256;
-    const uint16_t* src = qkv + r * ncol;
+    auto val = [&](int c) -> float {  // projection output, rounded to bf16 as the reference's q/k/v_proj
+        if constexpr (PART) {
+            float a = 0.f;
+            for (int z = 0; z < split; ++z) a += ws[z * slab + r * ncol + c];
+            return rbf(a);
+        } else {
+            return bf2f(qkv[r * ncol + c]);
+        }
+    };
     // pairs (d, d+128) of every rotated head: nh + nkv heads x 128 pairs
     for (int u = threadIdx.x; u < (nh + nkv) * 128; u += blockDim.x) {
         const int hh = u >> 7, d = u & 127;
-        const float a = bf2f(src[hh * 256 + d]), bb = bf2f(src[hh * 256 + d + 128]);
+        const float a = val(hh * 256 + d), bb = val(hh * 256 + d + 128);
         const float c = bf2f(cosT[p * 128 + d]), sn = bf2f(sinT[p * 128 + d]);
         const uint16_t oa = f2bf(rbf(a * c) + rbf(-bb * sn));
         const uint16_t ob = f2bf(rbf(bb * c) + rbf(a * sn));
@@ -254,15 +264,115 @@ __global__ void k_rope_kv(const uint16_t* __restrict__ qkv, int L, int nh, int n
         }
     }
     for (int u = threadIdx.x; u < nkv * 256; u += blockDim.x) {
-        vc[b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + u] = src[(nh + nkv) * 256 + u];
+        vc[b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + u] = f2bf(val((nh + nkv) * 256 + u));
     }
 }
 
-void rope_kv_append(hipStream_t s, const uint16_t* qkv, int B, int L, int nh, int nkv, const int64_t* pos,
-                    const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out, uint16_t* kcache,
-                    uint16_t* vcache, long kv_b_stride, int kv_start) {
-    hipLaunchKernelGGL(k_rope_kv, dim3(B * L), dim3(256), 0, s, qkv, L, nh, nkv, pos, cosT, sinT, max_pos, q_out,
-                       kcache, vcache, kv_b_stride, kv_start);
+void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int split, int B, int L, int nh, int nkv,
+                    const int64_t* pos, const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out,
+                    uint16_t* kcache, uint16_t* vcache, long kv_b_stride, int kv_start) {
+    const long slab = (long)B * L * (nh + 2 * nkv) * 256;
+    if (split > 1)
+        hipLaunchKernelGGL(k_rope_kv<true>, dim3(B * L), dim3(256), 0, s, qkv, ws, split, slab, L, nh, nkv, pos, cosT,
+                           sinT, max_pos, q_out, kcache, vcache, kv_b_stride, kv_start);
+    else
+        hipLaunchKernelGGL(k_rope_kv<false>, dim3(B * L), dim3(256), 0, s, qkv, ws, split, slab, L, nh, nkv, pos, cosT,
+                           sinT, max_pos, q_out, kcache, vcache, kv_b_stride, kv_start);
+}
+
+// ---------------------------------------------------------------- split-K reduce + residual + norm
+// Row per workgroup, 256 threads x 8 columns x 2 chunks (D <= 4096).
+template <bool LN>
+__global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict__ ws, int split, long slab,
+                                                         const uint16_t* __restrict__ bias, uint16_t* __restrict__ h,
+                                                         const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
+                                                         float eps, uint16_t* __restrict__ out, int D) {
+    __shared__ float red[4];
+    const long row = blockIdx.x;
+    float v[16];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int c = (threadIdx.x + it * 256) * 8;
+        if (c >= D) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[it * 8 + j] = 0.f;
+            continue;
+        }
+        uint4 hv = ldg16(h + row * D + c);
+        const uint16_t* he = reinterpret_cast<const uint16_t*>(&hv);
+        if (split > 1) {
+            float a[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = 0.f;
+            for (int z = 0; z < split; ++z) {
+                const f32x4 p0 = *reinterpret_cast<const f32x4*>(ws + z * slab + row * D + c);
+                const f32x4 p1 = *reinterpret_cast<const f32x4*>(ws + z * slab + row * D + c + 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { a[j] += p0[j]; a[4 + j] += p1[j]; }
+            }
+            uint4 bv = bias ? ldg16(bias + c) : make_uint4(0, 0, 0, 0);
+            const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
+            u16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float t = bias ? rbf(a[j] + bf2f(be[j])) : rbf(a[j]);
+                o.v[j] = f2bf(t + bf2f(he[j]));
+                v[it * 8 + j] = bf2f(o.v[j]);
+            }
+            *reinterpret_cast<u16x8*>(h + row * D + c) = o;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[it * 8 + j] = bf2f(he[j]);
+        }
+    }
+    float r, mu = 0.f;
+    if constexpr (LN) {
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += v[j];
+        mu = block_sum<256>(sum, red) / (float)D;
+        float sq = 0.f;
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+            if ((threadIdx.x + it * 256) * 8 < D)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { const float d = v[it * 8 + j] - mu; sq += d * d; }
+        r = 1.0f / sqrtf(block_sum<256>(sq, red) / (float)D + eps);
+    } else {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ss += v[j] * v[j];
+        r = 1.0f / sqrtf(block_sum<256>(ss, red) / (float)D + eps);
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int c = (threadIdx.x + it * 256) * 8;
+        if (c >= D) continue;
+        uint4 wv = ldg16(w + c);
+        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+        u16x8 o;
+        if constexpr (LN) {
+            uint4 bv = ldg16(b + c);
+            const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o.v[j] = f2bf((v[it * 8 + j] - mu) * r * bf2f(we[j]) + bf2f(be[j]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o.v[j] = f2bf((v[it * 8 + j] * r) * (1.0f + bf2f(we[j])));
+        }
+        *reinterpret_cast<u16x8*>(out + row * D + c) = o;
+    }
+}
+
+void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* bias, uint16_t* h, const uint16_t* w,
+                     const uint16_t* b, float eps, uint16_t* out, int rows, int D) {
+    const long slab = (long)rows * D;
+    if (b)
+        hipLaunchKernelGGL(k_splitk_res_norm<true>, dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, w, b, eps,
+                           out, D);
+    else
+        hipLaunchKernelGGL(k_splitk_res_norm<false>, dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, w, b, eps,
+                           out, D);
 }
 
 // ---------------------------------------------------------------- patch im2col

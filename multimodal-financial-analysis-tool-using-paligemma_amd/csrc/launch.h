@@ -30,9 +30,13 @@ struct EpiArgs {
 
 // C[M,N] = A[M,K] (row-major, lda) x W[N,K]^T (row-major, ldw).  For EPI_GEGLU the
 // "up" weight rows are W + up_offset_rows*ldw.  `ws` is fp32 scratch for split-K.
-void gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
-          Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0);
+// Returns the split-K factor used.  With defer = true and a split > 1 only the fp32 partial
+// slabs ws[split][M][N] are written and the epilogue is left to the consumer kernel
+// (splitk_res_norm / rope_kv_append); otherwise the epilogue is applied and 1 is returned.
+int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+         Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0, bool defer = false);
 size_t gemm_ws_bytes(int M, int N, int K);
+void gemm_force_plan(int cfg, int split);  // cfg < 0: automatic
 
 // ---------------------------------------------------------------- decode GEMV
 struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)
@@ -82,6 +86,11 @@ size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
 
 // ---------------------------------------------------------------- misc
+// Fused consumer of a projection + residual: if split > 1, h = bf16(bf16(sum_z ws[z] (+bias)) + h)
+// (fixed z order) is written back to h first; then out = norm(h): RMSNorm (b == nullptr,
+// (1 + w) form) or LayerNorm (b != nullptr).  D <= 4096.
+void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* bias, uint16_t* h, const uint16_t* w,
+                     const uint16_t* b, float eps, uint16_t* out, int rows, int D);
 void rmsnorm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, uint16_t* out, int rows, int D);
 void layernorm(hipStream_t s, const uint16_t* x, const uint16_t* w, const uint16_t* b, float eps, uint16_t* out,
                int rows, int D);
@@ -92,9 +101,10 @@ void merge_embed(hipStream_t s, const int64_t* ids, int B, int L, const uint16_t
                  const uint16_t* img, int n_img_rows, int64_t image_token, int64_t pad_id, float sqrt_h,
                  float normalizer, const uint16_t* embeds_in, int* scan_buf, uint16_t* out);
 void scale_rows(hipStream_t s, const uint16_t* x, long n, float normalizer, uint16_t* out);
-void rope_kv_append(hipStream_t s, const uint16_t* qkv, int B, int L, int nh, int nkv, const int64_t* pos,
-                    const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out, uint16_t* kcache,
-                    uint16_t* vcache, long kv_b_stride, int kv_start);
+// qkv: bf16 [B*L][(nh+2nkv)*256], or (split > 1) the fp32 partial slabs ws[split][B*L][...]
+void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int split, int B, int L, int nh, int nkv,
+                    const int64_t* pos, const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out,
+                    uint16_t* kcache, uint16_t* vcache, long kv_b_stride, int kv_start);
 void patchify(hipStream_t s, const void* px, int px_is_f32, int B, int C, int H, int W, int P, int Kpad,
               uint16_t* out);
 void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float scale, float offset);

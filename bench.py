@@ -212,7 +212,7 @@ def main():
     tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("gateup_hbm_bytes_per_launch")
+            traffic = json.load(open(tf))["gateup"]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
 

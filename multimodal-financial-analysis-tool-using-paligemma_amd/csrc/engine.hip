@@ -89,8 +89,8 @@ struct pgmi_ctx {
     size_t ws_bytes;
     // decode workspace
     uint16_t *dH, *dQ, *dAO, *dACT;
-    float *opart, *pmax, *dlogits;
-    int* pidx;
+    float *opart, *pmax, *dlogits, *amax_v;
+    int *pidx, *amax_i;
     int max_chunks;
     StepState* step;
     int64_t* d_ids;
@@ -413,6 +413,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->dlogits, (size_t)B * c.t_vocab))) return rc;
         if ((rc = dalloc_t(x, &x->pidx, (size_t)B * gemv_logits_blocks()))) return rc;
         if ((rc = dalloc_t(x, &x->step, 1))) return rc;
+        if ((rc = dalloc_t(x, &x->amax_v, (size_t)argmax_scratch_parts()))) return rc;
+        if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
     }
@@ -686,7 +688,9 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
 
 int pgmi_argmax(pgmi_ctx* x, const float* logits, int rows, int V, int64_t* out, void* stream) {
     if (!x || !logits || !out) return fail(PGMI_E_ARG, "null argument");
-    argmax_rows((hipStream_t)stream, logits, rows, V, out);
+    if (rows <= 0 || V <= 0) return fail(PGMI_E_ARG, "argmax: empty logits");
+    if (!x->amax_v) return fail(PGMI_E_STATE, "argmax scratch missing");
+    argmax_rows((hipStream_t)stream, logits, rows, V, x->amax_v, x->amax_i, out);
     LAUNCHCHK();
     return 0;
 }

@@ -19,7 +19,6 @@
 
 namespace pgmi {
 
-constexpr int VTS = 40;  // transposed-V LDS row stride (elements)
 
 template <int HD>
 struct HDInfo {
@@ -36,21 +35,27 @@ __device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool valid, in
     return __builtin_bit_cast(short8, ldg16(rowp + k));
 }
 
+typedef short s4v __attribute__((ext_vector_type(4)));
+
 template <int HD>
 __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
     using I = HDInfo<HD>;
+    constexpr int HDP = I::CT * 16;      // head dim padded to whole 16-column tiles
+    constexpr int VS = HDP + 16;         // V row stride in LDS (elements)
+    constexpr int CHK = 32;              // keys per P.V chunk
+    constexpr int VPT = (CHK * I::CH + 255) / 256;  // 16-B V chunks per thread per key chunk
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int LkP = (a.Lk + 31) & ~31;
     float* S = reinterpret_cast<float*>(smem_raw);                       // [16][LkP]
     uint16_t* P = reinterpret_cast<uint16_t*>(S + 16 * LkP);             // [16][LkP]
-    uint16_t* VT = P + 16 * LkP;                                         // [CT*16][VTS]
+    uint16_t* Vl = P + 16 * LkP;                                         // [2][CHK][VS]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.z, kvh = blockIdx.y;
     const int row0 = blockIdx.x * 16;
     const int nrows = a.Lq * a.G;
 
-    // ---- phase 1: S = bf16(bf16(Q K^T) * scale)
+    // ---- phase 1: S = bf16(bf16(Q K^T) * scale); K fragments of the next tile in flight
     const int qi = row0 + (lane & 15);
     const bool qvalid = qi < nrows;
     const int qpos = qvalid ? qi / a.G : 0, qhead = kvh * a.G + (qvalid ? qi % a.G : 0);
@@ -61,17 +66,33 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
 
     const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
     const int ntile = LkP / 16;
-    for (int t = wave; t < ntile; t += 4) {
+    auto kload = [&](int t, short8 (&kf)[I::KS]) {
         const int key = t * 16 + (lane & 15);
-        const bool kvalid = key < a.Lk;
-        const uint16_t* krow = kbase + (long)key * a.k_row_stride;
+        const uint16_t* krow = kbase + (long)(key < a.Lk ? key : 0) * a.k_row_stride;
+#pragma unroll
+        for (int kk = 0; kk < I::KS; ++kk) kf[kk] = load_frag<HD>(krow, key < a.Lk, kk, lane);
+    };
+    auto kcompute = [&](int t, const short8 (&kf)[I::KS]) {
+        const int key = t * 16 + (lane & 15);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < I::KS; ++kk) acc = mfma16(qf[kk], load_frag<HD>(krow, kvalid, kk, lane), acc);
+        for (int kk = 0; kk < I::KS; ++kk) acc = mfma16(qf[kk], kf[kk], acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = (lane >> 4) * 4 + r;
-            S[row * LkP + key] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
+            S[row * LkP + key] = key < a.Lk ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
+        }
+    };
+    {
+        short8 kA[I::KS], kB[I::KS];
+        int t = wave;
+        if (t < ntile) kload(t, kA);
+        for (; t < ntile; t += 8) {
+            if (t + 4 < ntile) kload(t + 4, kB);
+            kcompute(t, kA);
+            if (t + 4 >= ntile) break;
+            if (t + 8 < ntile) kload(t + 8, kA);
+            kcompute(t + 4, kB);
         }
     }
     __syncthreads();
@@ -90,39 +111,60 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
         sum = wave_sum(sum);
         for (int t = lane; t < LkP; t += 64) P[row * LkP + t] = t < a.Lk ? f2bf(S[row * LkP + t] / sum) : 0;
     }
-    __syncthreads();
 
-    // ---- phase 3: O = bf16(P V), V staged transposed 32 keys at a time
+    // ---- phase 3: O = bf16(P V); V chunks row-major in LDS (16-B stores), B fragments by
+    // ds_read_b64_tr_b16 (transposed read); the next chunk's rows are in flight meanwhile
     const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
+    uint4 vr[VPT];
+    auto vload = [&](int t0) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int e = tid + 256 * i;
+            const int tt = e / I::CH, ch = e % I::CH;
+            const int key = t0 + tt;
+            vr[i] = (e < CHK * I::CH && key < a.Lk) ? ldg16(vbase + (long)key * a.v_row_stride + ch * 8)
+                                                    : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto vstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int e = tid + 256 * i;
+            if (e < CHK * I::CH) {
+                const int tt = e / I::CH, ch = e % I::CH;
+                *reinterpret_cast<uint4*>(Vl + (buf * CHK + tt) * VS + ch * 8) = vr[i];
+            }
+        }
+        if constexpr (HDP != I::CH * 8) {  // zero the pad columns of the last tile
+            for (int e = tid; e < CHK; e += 256)
+                *reinterpret_cast<uint4*>(Vl + (buf * CHK + e) * VS + I::CH * 8) = make_uint4(0, 0, 0, 0);
+        }
+    };
     f32x4 oacc[(I::CT + 3) / 4];
 #pragma unroll
     for (int c = 0; c < (I::CT + 3) / 4; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t0 = 0; t0 < LkP; t0 += 32) {
-        for (int e = tid; e < 32 * I::CH; e += 256) {
-            const int tt = e / I::CH, ch = e % I::CH;
-            const int key = t0 + tt;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (key < a.Lk) v = ldg16(vbase + (long)key * a.v_row_stride + ch * 8);
-            const uint16_t* ve = reinterpret_cast<const uint16_t*>(&v);
+    const int nch = LkP / CHK;
+    vload(0);
+    const int g = lane >> 4, li = lane & 15;
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        vstore(buf);
+        if (c + 1 < nch) vload((c + 1) * CHK);
+        __syncthreads();  // V chunk (and, at c == 0, all of P) visible
+        const short8 pa = *reinterpret_cast<const short8*>(P + (lane & 15) * LkP + c * CHK + 8 * g);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) VT[(ch * 8 + j) * VTS + tt] = ve[j];
-        }
-        if constexpr ((HD % 16) != 0) {  // zero the pad columns of the last tile
-            for (int e = tid; e < (I::CT * 16 - I::CH * 8) * 32; e += 256) {
-                VT[(I::CH * 8 + e / 32) * VTS + (e % 32)] = 0;
-            }
-        }
-        __syncthreads();
-        const short8 pa = *reinterpret_cast<const short8*>(P + (lane & 15) * LkP + t0 + 8 * (lane >> 4));
-#pragma unroll
-        for (int c = 0; c < (I::CT + 3) / 4; ++c) {
-            const int ct = wave + 4 * c;
+        for (int cc = 0; cc < (I::CT + 3) / 4; ++cc) {
+            const int ct = wave + 4 * cc;
             if (ct < I::CT) {
-                const short8 vb = *reinterpret_cast<const short8*>(VT + (ct * 16 + (lane & 15)) * VTS + 8 * (lane >> 4));
-                oacc[c] = mfma16(pa, vb, oacc[c]);
+                const uint16_t* vp = Vl + (buf * CHK + 8 * g + (li >> 2)) * VS + ct * 16 + 4 * (li & 3);
+                const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s4v*)(vp));
+                const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s4v*)(vp + 4 * VS));
+                const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                oacc[cc] = mfma16(pa, vb, oacc[cc]);
             }
         }
-        __syncthreads();
     }
 #pragma unroll
     for (int c = 0; c < (I::CT + 3) / 4; ++c) {
@@ -142,8 +184,8 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
 
 static size_t attn_full_lds(int head_dim, int Lk) {
     const int LkP = (Lk + 31) & ~31;
-    const int ct = (head_dim + 15) / 16;
-    return (size_t)16 * LkP * 4 + (size_t)16 * LkP * 2 + (size_t)ct * 16 * VTS * 2;
+    const int hdp = (head_dim + 15) / 16 * 16;
+    return (size_t)16 * LkP * 4 + (size_t)16 * LkP * 2 + (size_t)2 * 32 * (hdp + 16) * 2;
 }
 
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
@@ -169,8 +211,8 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
 }
 
 int attention_prefill_max_keys(int head_dim) {
-    const int ct = (head_dim + 15) / 16;
-    return (int)((160 * 1024 - (size_t)ct * 16 * VTS * 2) / (16 * 6)) & ~31;
+    const int hdp = (head_dim + 15) / 16 * 16;
+    return (int)((160 * 1024 - (size_t)2 * 32 * (hdp + 16) * 2) / (16 * 6)) & ~31;
 }
 
 // ================================================================ decode (Lq = 1)

@@ -6,6 +6,8 @@
 //   embed/merge    Embedding + merge + x sqrt(hidden)   modeling_gemma.py:565,468-537,367-368
 //   rope_kv_append rotary + KVCache.update modeling_gemma.py:143-199,259, :10-36
 //   patchify       Conv2d(k=s=14) as im2col (+ pixel cast to bf16)  modeling_siglip.py:45-51,67; modeling_gemma.py:570
+#include <algorithm>
+
 #include "common.h"
 #include "launch.h"
 
@@ -443,36 +445,64 @@ void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int
     hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out);
 }
 
-// torch.argmax over each row of x [rows][V] (first max wins)
-__global__ void k_argmax_rows(const float* __restrict__ x, int V, int64_t* __restrict__ out) {
-    const float* xr = x + (long)blockIdx.x * V;
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) {
-        const float v = xr[i];
-        if (v > best) { best = v; bi = i; }
-    }
-    __shared__ float sv[256];
-    __shared__ int si[256];
-    sv[threadIdx.x] = best;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            const float v = sv[threadIdx.x + o];
-            const int ix = si[threadIdx.x + o];
-            if (v > sv[threadIdx.x] || (v == sv[threadIdx.x] && ix < si[threadIdx.x])) {
-                sv[threadIdx.x] = v;
-                si[threadIdx.x] = ix;
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[blockIdx.x] = si[0];
+// torch.argmax over each row of x [rows][V] (first max wins).  Stage 1: a (nb x rows) grid, each
+// block scans a contiguous slice of a row with 16-B loads and leaves (max, first index); stage 2
+// (k_argmax_finish) reduces the nb partials of each row.  nb == 1 writes the answer directly.
+__device__ __forceinline__ void amax_take(float v, int i, float& best, int& bi) {
+    if (v > best || (v == best && i < bi)) { best = v; bi = i; }
 }
 
-void argmax_rows(hipStream_t s, const float* x, int rows, int V, int64_t* out) {
-    hipLaunchKernelGGL(k_argmax_rows, dim3(rows), dim3(256), 0, s, x, V, out);
+__global__ void k_argmax_part(const float* __restrict__ x, int V, int slice, float* __restrict__ pmax,
+                              int* __restrict__ pidx, int64_t* __restrict__ out) {
+    const int row = blockIdx.y, nb = gridDim.x;
+    const float* xr = x + (long)row * V;
+    const int lo = blockIdx.x * slice, hi = min(V, lo + slice);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    const bool vec = ((V & 3) == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+    if (vec) {
+        for (int i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + i);
+            amax_take(v.x, i, best, bi);
+            amax_take(v.y, i + 1, best, bi);
+            amax_take(v.z, i + 2, best, bi);
+            amax_take(v.w, i + 3, best, bi);
+        }
+    } else {
+        for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) amax_take(xr[i], i, best, bi);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float v = __shfl_xor(best, o, 64);
+        const int ix = __shfl_xor(bi, o, 64);
+        amax_take(v, ix, best, bi);
+    }
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    if ((threadIdx.x & 63) == 0) {
+        sv[threadIdx.x >> 6] = best;
+        si[threadIdx.x >> 6] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) amax_take(sv[w], si[w], best, bi);
+        if (nb == 1) {
+            out[row] = bi;
+        } else {
+            pmax[(long)row * nb + blockIdx.x] = best;
+            pidx[(long)row * nb + blockIdx.x] = bi;
+        }
+    }
+}
+
+int argmax_scratch_parts() { return 1024; }
+
+void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, int* pidx, int64_t* out) {
+    int nb = rows >= argmax_scratch_parts() ? 1 : argmax_scratch_parts() / rows;
+    nb = std::max(1, std::min(nb, std::min(128, (V + 2047) / 2048)));
+    const int slice = ((V + nb - 1) / nb + 3) & ~3;
+    nb = (V + slice - 1) / slice;
+    hipLaunchKernelGGL(k_argmax_part, dim3(nb, rows), dim3(256), 0, s, x, V, slice, pmax, pidx, out);
+    if (nb > 1) hipLaunchKernelGGL(k_argmax_finish, dim3(rows), dim3(256), 0, s, pmax, pidx, nb, out);
 }
 
 // ---------------------------------------------------------------- synthetic weights (bench / tests)

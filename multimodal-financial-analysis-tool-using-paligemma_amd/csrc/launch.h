@@ -59,7 +59,8 @@ int gemv_logits_blocks();
 void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts);
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out);
-void argmax_rows(hipStream_t s, const float* x, int rows, int V, int64_t* out);
+int argmax_scratch_parts();
+void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, int* pidx, int64_t* out);
 
 // ---------------------------------------------------------------- attention
 struct AttnArgs {

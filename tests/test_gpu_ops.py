@@ -183,3 +183,28 @@ def test_synthetic_fill_matches_oracle(eng):
         ref = W.gen_bf16(name, tuple(view.shape), 1234)
         got = view.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
         assert np.array_equal(got, ref), name
+
+
+@pytest.mark.parametrize("rows,V", [(1, 257216), (2, 257216), (3, 1001), (1, 7), (40, 16384), (1500, 300)])
+def test_argmax_rows(eng, rows, V):
+    """pgmi_argmax == torch.argmax (first maximum wins), with planted ties."""
+    g = torch.Generator().manual_seed(rows * 7 + V)
+    x = torch.randn(rows, V, generator=g)
+    # plant ties of the row maximum at two positions; the earlier must win
+    for r in range(rows):
+        m = float(x[r].max()) + 1.0
+        i, j = sorted(torch.randint(0, V, (2,), generator=g).tolist())
+        x[r, j] = m
+        x[r, i] = m
+    xd = x.cuda()
+    got = eng.argmax(xd).cpu()
+    assert torch.equal(got, x.argmax(-1))
+    # unaligned view (offset by one float): exercises the scalar path
+    if V > 8:
+        y = torch.randn(rows * V + 1, generator=g)
+        yd = y.cuda()[1:].view(rows, V)
+        got = torch.empty(rows, dtype=torch.int64, device="cuda")
+        from pgmi import _native as N
+        N.check(eng.lib.pgmi_argmax(eng.ctx, yd.data_ptr(), rows, V, got.data_ptr(), N.stream_handle()))
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), y[1:].view(rows, V).argmax(-1))

@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--prefill-iters", type=int, default=20)
     ap.add_argument("--kernel-iters", type=int, default=90)
-    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     return ap.parse_args()

@@ -100,46 +100,53 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
         // (G <= 8 query heads of one KV head: PaliGemma's MQA, checked at pgmi_create)
         // x[b][h*256 + d] = bf16(sum_c e^(m_c - M) O_c[h][d] / sum_c e^(m_c - M) l_c), chunks in
         // a fixed order (the flash-decoding combine of k_attn_decode's partials)
+        // every thread combines its own 8 outputs from the chunk records directly (stats and
+        // partial rows in one round trip, no LDS staging of the weights, no barrier)
         const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
-        float* wm = reinterpret_cast<float*>(xs + B * K);  // [B][nch][8]: m_c, then weights
-        float* wl = wm + B * a.max_chunks * 8;            // [B][nch][8]: l_c
-        float* inv = wl + B * a.max_chunks * 8;           // [B][8]: sum_c w_c l_c
-        for (int i = tid; i < a.nb * nch * 8; i += 256) {
-            const int b = i / (nch * 8), c = (i / 8) % nch, h = i & 7;
-            const float* st_c = a.part + ((long)b * a.max_chunks + c) * kAttnPartStride + 16 * 256;
-            wm[(b * a.max_chunks + c) * 8 + h] = st_c[h];
-            wl[(b * a.max_chunks + c) * 8 + h] = st_c[16 + h];
-        }
-        __syncthreads();
-        if (tid < a.nb * 8) {
-            const int b = tid >> 3, h = tid & 7;
-            float M = -INFINITY;
-            for (int c = 0; c < nch; ++c) M = fmaxf(M, wm[(b * a.max_chunks + c) * 8 + h]);
-            float S = 0.f;
-            for (int c = 0; c < nch; ++c) {
-                const float w = expf(wm[(b * a.max_chunks + c) * 8 + h] - M);
-                wm[(b * a.max_chunks + c) * 8 + h] = w;
-                S += w * wl[(b * a.max_chunks + c) * 8 + h];
-            }
-            inv[b * 8 + h] = S;
-        }
-        __syncthreads();
-        for (int e8 = tid; e8 < a.nb * K / 8; e8 += 256) {
+        constexpr int CMAX = 8;  // chunks held in registers; longer caches take two passes
+        const int nitems = a.nb * K / 8;
+        for (int e8 = tid; e8 < nitems; e8 += 256) {
             const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
-            const int h = e >> 8, d = e & 255;
+            const int h = e >> 8;
+            const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + (e & 255);
+            const float* sp = a.part + (long)b * a.max_chunks * kAttnPartStride + 16 * 256 + h;
             float o[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] = 0.f;
-            const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + d;
-#pragma unroll 4
-            for (int c = 0; c < nch; ++c) {
-                const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
-                const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
-                const float w = wm[(b * a.max_chunks + c) * 8 + h];
+            float M = -INFINITY, S = 0.f;
+            if (nch <= CMAX) {
+                f32x4 x0[CMAX], x1[CMAX];
+                float mc[CMAX], lc[CMAX];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
+                for (int c = 0; c < CMAX; ++c)
+                    if (c < nch) {
+                        x0[c] = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+                        x1[c] = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+                        mc[c] = sp[(long)c * kAttnPartStride];
+                        lc[c] = sp[(long)c * kAttnPartStride + 16];
+                    }
+#pragma unroll
+                for (int c = 0; c < CMAX; ++c)
+                    if (c < nch) M = fmaxf(M, mc[c]);
+#pragma unroll
+                for (int c = 0; c < CMAX; ++c)
+                    if (c < nch) {
+                        const float w = expf(mc[c] - M);
+                        S += w * lc[c];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) { o[j] += w * x0[c][j]; o[4 + j] += w * x1[c][j]; }
+                    }
+            } else {
+                for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
+                for (int c = 0; c < nch; ++c) {
+                    const float w = expf(sp[(long)c * kAttnPartStride] - M);
+                    S += w * sp[(long)c * kAttnPartStride + 16];
+                    const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+                    const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
+                }
             }
-            const float S = inv[b * 8 + h];
             u16x8 ob;
 #pragma unroll
             for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(o[j] / S);
@@ -156,6 +163,9 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
             for (int c = 0; c < KCW; ++c)
                 xr[b][c] = (b < a.nb) ? ldg16(a.x + (long)b * K + kofs + 512 * c) : make_uint4(0, 0, 0, 0);
         if (a.norm_w) {  // WK == 1: the wave holds the whole row
+            uint4 nw[KCW];  // norm weights in the same round trip as the activation
+#pragma unroll
+            for (int c = 0; c < KCW; ++c) nw[c] = ldg16(a.norm_w + kofs + 512 * c);
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 float ss = 0.f;
@@ -169,8 +179,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
                 const float r = 1.0f / sqrtf(ss / (float)K + a.eps);
 #pragma unroll
                 for (int c = 0; c < KCW; ++c) {
-                    const uint4 wv = ldg16(a.norm_w + kofs + 512 * c);
-                    const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+                    const uint16_t* we = reinterpret_cast<const uint16_t*>(&nw[c]);
                     const uint16_t* e = reinterpret_cast<const uint16_t*>(&xr[b][c]);
                     u16x8 o;
 #pragma unroll
@@ -237,6 +246,22 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     for (int b = 0; b < B; ++b) { best[b] = -INFINITY; besti[b] = 0x7fffffff; }
 
     while (bb < a.n_units) {
+        // epilogue operands of this group (residual h, RoPE cos/sin), queued behind its weights
+        float pre[RPW][B][2];
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int u = ub + i < a.n_units ? ub + i : a.n_units - 1;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const int bq = b < a.nb ? b : a.nb - 1;
+                if constexpr (MODE == GV_RES || MODE == GV_ORES) {
+                    pre[i][b][0] = bf2f(a.out[(long)bq * a.n_units + u]);
+                } else if constexpr (MODE == GV_QKV) {
+                    pre[i][b][0] = bf2f(a.cosT[(long)pos * 128 + (u & 127)]);
+                    pre[i][b][1] = bf2f(a.sinT[(long)pos * 128 + (u & 127)]);
+                }
+            }
+        }
         float acc[RPW][NR][B];
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
@@ -303,8 +328,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
                 if (b >= a.nb) break;
                 if constexpr (MODE == GV_RES || MODE == GV_ORES) {
                     if (lane == 0) {
-                        uint16_t* hp = a.out + (long)b * a.n_units + u;
-                        *hp = f2bf(rbf(acc[i][0][b]) + bf2f(*hp));
+                        a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[i][0][b]) + pre[i][b][0]);
                     }
                 } else if constexpr (MODE == GV_GEGLU) {
                     if (lane == 0) {
@@ -321,8 +345,8 @@ __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
                         const float x0 = rbf(acc[i][0][b]), x1 = rbf(acc[i][1][b]);
                         const int nh = a.I;
                         if (hh < nh + a.nkv) {
-                            const float c = bf2f(a.cosT[(long)pos * 128 + d]);
-                            const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
+                            const float c = pre[i][b][0];
+                            const float sn = pre[i][b][1];
                             const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
                             const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sn));
                             uint16_t* dst;
@@ -373,7 +397,6 @@ template <int B, int KCH, int RPW, int MODE, int WK = 1>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
     constexpr bool XREG = (MODE != GV_ORES) && B * (KCH / WK) <= 8;
     size_t lds = XREG ? 0 : (size_t)B * KCH * 512 * sizeof(uint16_t);
-    if (MODE == GV_ORES) lds += ((size_t)B * a.max_chunks * 16 + B * 8) * sizeof(float);
     static size_t attr = 0;  // largest dynamic LDS size granted so far
     if (lds > attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG>),

@@ -1,0 +1,147 @@
+#pragma once
+// attn_decode_body.h -- flash-decoding workgroup body (standalone kernel: kernels_attn.hip;
+// fused decode step: kernels_step.hip).
+//
+// Workgroup c owns keys [64c, 64c+64) of one (b, kv head) for all G query heads.  Scores are
+// rounded exactly as the reference (bf16(bf16(q.k) * scale), modeling_gemma.py:262-266); each
+// chunk writes (m_c, l_c = sum e^(s - m_c), O_c = sum e^(s - m_c) v) in fp32.  The combine
+// o = bf16(sum_c e^(m_c - M) O_c / sum_c e^(m_c - M) l_c), in a fixed chunk order, is the
+// prologue of the o_proj GEMV that consumes o (gemv_body.h, GV_ORES).
+// P.V runs on MFMA from bf16 e = exp(s - m_c) (the reference rounds the normalised p to bf16,
+// modeling_gemma.py:273,277; here the unnormalised chunk-local e is rounded, the fp32 sum l_c
+// normalises at the combine: same rounding granularity, documented in DESIGN.md).
+// F (fused step): the cache rows written before this launch are fetched BEFORE waiting for the
+// q/k/v phase; q and the new row (index kv_len) are read coherently after it.
+#include "coh.h"
+#include "common.h"
+#include "launch.h"
+
+namespace pgmi {
+
+constexpr int DCH = 64;                 // keys per chunk
+constexpr int PSTRIDE = 16 * 256 + 32;  // per-chunk partial record: O_c[16][256], m_c[16], l_c[16]
+constexpr int DVS = 256 + 16;           // V row stride in LDS (elements): tr16 reads 2-way at most
+constexpr int DPS = DCH + 8;            // P row stride in LDS (elements)
+constexpr int kAttnDecodeLds = DCH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2 + 2 * 16 * 4;
+
+typedef short s4v_t __attribute__((ext_vector_type(4)));
+
+template <bool C>
+__device__ __forceinline__ short8 frag256(const uint16_t* rowp, bool valid, int kk, int lane) {
+    const int k = 32 * kk + 8 * (lane >> 4);
+    if (!valid) return short8{0, 0, 0, 0, 0, 0, 0, 0};
+    return __builtin_bit_cast(short8, ldx16<C>(rowp + k));
+}
+
+template <bool F>
+__device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
+                                                  int max_chunks, int chunk, int kvh, int b, unsigned char* lds,
+                                                  const Dep& dep) {
+    const int kv_len = st->kv_len;
+    const int Lk = kv_len + 1;
+    const int nch = (Lk + DCH - 1) / DCH;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (chunk >= nch) return;  // (fused: no arrival; the consumer waits for nch chunks)
+    const int t0 = chunk * DCH;
+    const int nk = (Lk - t0) < DCH ? (Lk - t0) : DCH;
+    uint16_t* Vs = reinterpret_cast<uint16_t*>(lds);                          // [DCH][DVS]
+    float (*S)[DCH + 4] = reinterpret_cast<float (*)[DCH + 4]>(lds + DCH * DVS * 2);
+    uint16_t* Ps = reinterpret_cast<uint16_t*>(lds + DCH * DVS * 2 + 16 * (DCH + 4) * 4);
+    float (*stat)[16] = reinterpret_cast<float (*)[16]>(lds + DCH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2);
+
+    // rows already in the cache before this step (F: the new row kv_len comes after the wait)
+    const int n_old = F ? (kv_len - t0 < nk ? kv_len - t0 : nk) : nk;
+    const uint16_t* vb = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
+    uint4 vr[DCH * 32 / 256];
+#pragma unroll
+    for (int i = 0; i < DCH * 32 / 256; ++i) {
+        const int e = tid + 256 * i, r = e >> 5, c = e & 31;
+        vr[i] = r < n_old ? ldg16(vb + (long)(t0 + r) * a.v_row_stride + 8 * c) : make_uint4(0, 0, 0, 0);
+    }
+    const int qi = lane & 15;
+    const bool qvalid = qi < a.G;
+    const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
+    const int key = t0 + wave * 16 + (lane & 15);
+    const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
+    short8 qf[8], kf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<false>(krow, key < (F ? kv_len : Lk), kk, lane);
+
+    if constexpr (F) {
+        dep_wait(dep);
+        if (key == kv_len) {
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<true>(krow, true, kk, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < DCH * 32 / 256; ++i) {
+            const int e = tid + 256 * i, r = e >> 5, c = e & 31;
+            if (t0 + r == kv_len) vr[i] = ld16_coh(vb + (long)kv_len * a.v_row_stride + 8 * c);
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256<F>(qrow, qvalid, kk, lane);
+
+    // ---- scores (MFMA): wave w -> keys t0 + 16w + (lane & 15)
+    {
+        const bool kvalid = key < Lk;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) acc = mfma16(qf[kk], kf[kk], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < DCH * 32 / 256; ++i) {
+        const int e = tid + 256 * i, r = e >> 5, c = e & 31;
+        *reinterpret_cast<uint4*>(Vs + r * DVS + 8 * c) = vr[i];
+    }
+    __syncthreads();
+    // ---- chunk-local max / exp / sum: wave w handles head rows 4w..4w+3, lane = key
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int h = wave * 4 + rr;
+        const float sv = S[h][lane];
+        const float m = wave_max(sv);
+        const float e = (lane < nk && h < a.G) ? expf(sv - m) : 0.f;
+        Ps[h * DPS + lane] = f2bf(e);
+        const float l = wave_sum(e);
+        if (lane == 0) { stat[0][h] = m; stat[1][h] = l; }
+    }
+    __syncthreads();
+    // ---- O_c[h][d] = sum_t e[h][t] v[t][d] (MFMA): wave w -> d tiles 4w..4w+3; B operand by
+    // ds_read_b64_tr_b16 from the row-major V image
+    float* pb = part + ((long)(b * a.n_kv + kvh) * max_chunks + chunk) * PSTRIDE;
+    {
+        const int g = lane >> 4, li = lane & 15;
+        short8 pa[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) pa[kk] = *reinterpret_cast<const short8*>(Ps + li * DPS + 32 * kk + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ct = wave * 4 + j;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const uint16_t* vp = Vs + (32 * kk + 8 * g + (li >> 2)) * DVS + ct * 16 + 4 * (li & 3);
+                const s4v_t lo =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v_t*)(vp));
+                const s4v_t hi =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v_t*)(vp + 4 * DVS));
+                const short8 vbf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                acc = mfma16(pa[kk], vbf, acc);
+            }
+            // C map: col d = ct*16 + (lane & 15), row h = (lane >> 4)*4 + r
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int h = (lane >> 4) * 4 + r;
+                if (h < a.G) stxf<F>(pb + h * 256 + ct * 16 + li, acc[r]);
+            }
+        }
+    }
+    if (tid < 32) stxf<F>(pb + 16 * 256 + tid, stat[tid >> 4][tid & 15]);
+    if constexpr (F) dep_arrive(dep);
+}
+
+}  // namespace pgmi

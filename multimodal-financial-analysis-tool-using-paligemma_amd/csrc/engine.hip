@@ -7,6 +7,7 @@
 //   decode   one inference.py loop iteration    inference.py:56-78
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -48,13 +49,15 @@ struct Slot {
 };
 
 struct GraphKey {
+    int fused;
     int B;
     void* kv;
     int kv_batch, kv_max;
     float* logits;
     int64_t* next;
     bool operator<(const GraphKey& o) const {
-        return std::tie(B, kv, kv_batch, kv_max, logits, next) < std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next);
+        return std::tie(fused, B, kv, kv_batch, kv_max, logits, next) <
+               std::tie(o.fused, o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next);
     }
 };
 
@@ -94,6 +97,10 @@ struct pgmi_ctx {
     int max_chunks;
     StepState* step;
     int64_t* d_ids;
+    int64_t* d_next;             // argmax target when the caller passes none
+    unsigned* step_sync = nullptr;  // fused decode step: phase counters (zeroed per launch)
+    unsigned* step_err = nullptr;   // fused decode step: sticky status
+    bool fused = true;              // batch-1 decode as one dataflow launch (kernels_step.hip)
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
 };
@@ -261,6 +268,7 @@ int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
     if (c.max_batch < 1 || c.max_batch > 8) return fail(PGMI_E_ARG, "max_batch must be in [1, 8]");
     if (c.v_hidden > 4096) return fail(PGMI_E_ARG, "v_hidden too large for the LayerNorm kernel");
     auto* x = new pgmi_ctx();
+    if (const char* v = std::getenv("PGMI_DECODE_FUSED")) x->fused = std::strcmp(v, "0") != 0;
     x->c = c;
     if (x->c.max_kv <= 0) x->c.max_kv = c.t_max_pos;
     x->device = device;
@@ -416,6 +424,11 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->amax_v, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
+        if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
+        if ((rc = dalloc_t(x, &x->step_sync, (size_t)decode_step_sync_words(c.t_layers)))) return rc;
+        if ((rc = dalloc_t(x, &x->step_err, 4))) return rc;
+        HIPCHK(hipMemset(x->step_err, 0, 4 * sizeof(unsigned)));
+        HIPCHK(hipMemset(x->step_sync, 0, (size_t)decode_step_sync_words(c.t_layers) * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
     }
     // derived tensors
@@ -648,6 +661,68 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     return 0;
 }
 
+static bool fused_ok(const pgmi_ctx* x, int B) {
+    const pgmi_config& c = x->c;
+    return x->fused && B == 1 && c.t_layers <= 28 && c.t_intermediate == 16384 && c.t_hidden == 2048 &&
+           c.t_head_dim == 256 && c.t_heads + 2 * c.t_kv_heads <= 16;
+}
+
+// batch-1 step as one dataflow launch (kernels_step.hip); same arithmetic as decode_body
+static int decode_fused(pgmi_ctx* x, hipStream_t s, const int64_t* ids, void* kv, int kv_batch, int kv_max,
+                        float* logits, int64_t* next_ids) {
+    const pgmi_config& c = x->c;
+    const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
+    const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
+    uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
+    DecodeStepDesc d{};
+    d.layers = c.t_layers;
+    for (int i = 0; i < c.t_layers; ++i) {
+        d.ln1[i] = TL(x, i, "input_layernorm.weight");
+        d.wqkv[i] = TL(x, i, "self_attn.q_proj.weight");
+        d.wo[i] = TL(x, i, "self_attn.o_proj.weight");
+        d.ln2[i] = TL(x, i, "post_attention_layernorm.weight");
+        d.wgu[i] = TL(x, i, "mlp.gate_proj.weight");
+        d.wdn[i] = TL(x, i, "mlp.down_proj.weight");
+        d.kc[i] = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
+        d.vc[i] = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+    }
+    d.ids = ids;
+    d.E = W(x, "language_model.model.embed_tokens.weight");
+    d.fnorm = W(x, "language_model.model.norm.weight");
+    d.normalizer = bf16_round_host(std::sqrt((float)H));
+    d.eps = c.t_rms_eps;
+    d.scale = 1.0f / std::sqrt((float)HD);
+    d.pad_id = c.pad_token_id;
+    d.cosT = x->cosT; d.sinT = x->sinT; d.max_pos = c.t_max_pos; d.st = x->step;
+    d.h = x->dH; d.q = x->dQ; d.act = x->dACT; d.part = x->opart; d.max_chunks = x->max_chunks; d.kvb = kvb;
+    d.nh = NH; d.nkv = NKV; d.H = H; d.I = c.t_intermediate; d.V = c.t_vocab;
+    d.logits = logits; d.pmax = x->pmax; d.pidx = x->pidx; d.next = next_ids ? next_ids : x->d_next;
+    d.sync = x->step_sync; d.err = x->step_err;
+    if (decode_step_launch(s, d)) return fail(PGMI_E_HIP, "fused decode step launch failed");
+    return 0;
+}
+
+static int decode_any(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
+                      int launch_keys, float* logits, int64_t* next_ids) {
+    if (fused_ok(x, B)) return decode_fused(x, s, ids, kv, kv_batch, kv_max, logits, next_ids);
+    return decode_body(x, s, ids, B, kv, kv_batch, kv_max, launch_keys, logits, next_ids);
+}
+
+int pgmi_set_decode_fused(pgmi_ctx* x, int on) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    x->fused = on != 0;
+    return 0;
+}
+
+int pgmi_decode_status(pgmi_ctx* x, unsigned* status) {
+    if (!x || !status) return fail(PGMI_E_ARG, "null argument");
+    HIPCHK(hipMemcpy(status, x->step_err, sizeof(unsigned), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(x->step_err, 0, sizeof(unsigned)));
+    // a step that timed out may have left counters armed: start the next one from zero
+    if (*status) HIPCHK(hipMemset(x->step_sync, 0, (size_t)decode_step_sync_words(x->c.t_layers) * sizeof(unsigned)));
+    return 0;
+}
+
 int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len, int position,
                 float* logits, int64_t* next_ids, int use_graph, void* stream) {
     int rc;
@@ -660,24 +735,25 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     hipStream_t s = (hipStream_t)stream;
     set_step(s, x->step, kv_len, position);
     if (!use_graph) {
-        decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids);
+        if ((rc = decode_any(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids))) return rc;
         LAUNCHCHK();
         return 0;
     }
     HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids};
+    GraphKey key{fused_ok(x, B) ? 1 : 0, B, kv, kv_batch, kv_max, logits, next_ids};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            decode_body(x, s, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+            if ((rc = decode_any(x, s, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
             LAUNCHCHK();
             return 0;
         }
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        decode_body(x, x->cap_stream, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+        rc = decode_any(x, x->cap_stream, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
+        if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
     }

@@ -14,6 +14,7 @@
 // transposed in LDS 32 keys at a time for the PV MFMA.
 // Decode (Lq = 1): keys split over 64-key chunks across workgroups (flash-decoding), in three
 // short kernels: scores -> (global max/sum, P, partial P.V) -> fixed-order combine.
+#include "attn_decode_body.h"
 #include "common.h"
 #include "launch.h"
 
@@ -35,7 +36,7 @@ __device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool valid, in
     return __builtin_bit_cast(short8, ldg16(rowp + k));
 }
 
-typedef short s4v __attribute__((ext_vector_type(4)));
+typedef s4v_t s4v;
 
 template <int HD>
 __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
@@ -216,112 +217,11 @@ int attention_prefill_max_keys(int head_dim) {
 }
 
 // ================================================================ decode (Lq = 1)
-// Flash-decoding: workgroup c owns keys [64c, 64c+64) of one (b, kv head) for all G query
-// heads.  Scores are rounded exactly as the reference (bf16(bf16(q.k) * scale)); each chunk
-// writes (m_c, l_c = sum e^(s - m_c), O_c = sum e^(s - m_c) v) in fp32.  The combine
-// o = bf16(sum_c e^(m_c - M) O_c / sum_c e^(m_c - M) l_c), in a fixed chunk order, is the
-// prologue of the o_proj GEMV that consumes o (kernels_gemv.hip, GV_ORES): no inter-workgroup
-// hand-off inside this kernel, the kernel boundary orders it.
-// P.V runs on MFMA from bf16 e = exp(s - m_c) (the reference rounds the normalised p to bf16,
-// modeling_gemma.py:273,277; here the unnormalised chunk-local e is rounded, the fp32 sum l_c
-// normalises at the combine: same rounding granularity, documented in DESIGN.md).
-constexpr int DCH = 64;                 // keys per chunk
-constexpr int PSTRIDE = 16 * 256 + 32;  // per-chunk partial record: O_c[16][256], m_c[16], l_c[16]
-constexpr int DVS = 256 + 16;           // V row stride in LDS (elements): tr16 reads 2-way at most
-constexpr int DPS = DCH + 8;            // P row stride in LDS (elements)
-
+// flash-decoding body: attn_decode_body.h
 __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a, const StepState* st, float* __restrict__ part,
                                                       int max_chunks) {
-    const int Lk = st->kv_len + 1;
-    const int nch = (Lk + DCH - 1) / DCH;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b = blockIdx.z, kvh = blockIdx.y, chunk = blockIdx.x;
-    if (chunk >= nch) return;
-    const int t0 = chunk * DCH;
-    const int nk = (Lk - t0) < DCH ? (Lk - t0) : DCH;
-    __shared__ __attribute__((aligned(16))) uint16_t Vs[DCH * DVS];   // V chunk, row-major
-    __shared__ __attribute__((aligned(16))) float S[16][DCH + 4];     // scores
-    __shared__ __attribute__((aligned(16))) uint16_t Ps[16 * DPS];    // bf16 e, rows >= G zero
-    __shared__ float stat[2][16];
-
-    // V rows of the chunk first (16-B loads, row-major, rows past the cache zero)
-    const uint16_t* vb = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
-    uint4 vr[DCH * 32 / 256];
-#pragma unroll
-    for (int i = 0; i < DCH * 32 / 256; ++i) {
-        const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        vr[i] = r < nk ? ldg16(vb + (long)(t0 + r) * a.v_row_stride + 8 * c) : make_uint4(0, 0, 0, 0);
-    }
-
-    // ---- scores (MFMA): wave w -> keys t0 + 16w + (lane & 15)
-    {
-        const int qi = lane & 15;
-        const bool qvalid = qi < a.G;
-        const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
-        const int key = t0 + wave * 16 + (lane & 15);
-        const bool kvalid = key < Lk;
-        const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
-        short8 qf[8], kf[8];
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-            qf[kk] = load_frag<256>(qrow, qvalid, kk, lane);
-            kf[kk] = load_frag<256>(krow, kvalid, kk, lane);
-        }
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc = mfma16(qf[kk], kf[kk], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
-    }
-#pragma unroll
-    for (int i = 0; i < DCH * 32 / 256; ++i) {
-        const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        *reinterpret_cast<uint4*>(Vs + r * DVS + 8 * c) = vr[i];
-    }
-    __syncthreads();
-    // ---- chunk-local max / exp / sum: wave w handles head rows 4w..4w+3, lane = key
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int h = wave * 4 + rr;
-        const float sv = S[h][lane];
-        const float m = wave_max(sv);
-        const float e = (lane < nk && h < a.G) ? expf(sv - m) : 0.f;
-        Ps[h * DPS + lane] = f2bf(e);
-        const float l = wave_sum(e);
-        if (lane == 0) { stat[0][h] = m; stat[1][h] = l; }
-    }
-    __syncthreads();
-    // ---- O_c[h][d] = sum_t e[h][t] v[t][d] (MFMA): wave w -> d tiles 4w..4w+3; B operand by
-    // ds_read_b64_tr_b16 from the row-major V image
-    float* pb = part + ((long)(b * a.n_kv + kvh) * max_chunks + chunk) * PSTRIDE;
-    {
-        const int g = lane >> 4, li = lane & 15;
-        short8 pa[2];
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) pa[kk] = *reinterpret_cast<const short8*>(Ps + li * DPS + 32 * kk + 8 * g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int ct = wave * 4 + j;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                const uint16_t* vp = Vs + (32 * kk + 8 * g + (li >> 2)) * DVS + ct * 16 + 4 * (li & 3);
-                const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vp));
-                const s4v hi =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vp + 4 * DVS));
-                const short8 vbf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                acc = mfma16(pa[kk], vbf, acc);
-            }
-            // C map: col d = ct*16 + (lane & 15), row h = (lane >> 4)*4 + r
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int h = (lane >> 4) * 4 + r;
-                if (h < a.G) pb[h * 256 + ct * 16 + li] = acc[r];
-            }
-        }
-    }
-    if (tid < 32) pb[16 * 256 + tid] = stat[tid >> 4][tid & 15];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
+    attn_decode_block<false>(a, st, part, max_chunks, blockIdx.x, blockIdx.y, blockIdx.z, lds, Dep{});
 }
 
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks) {

@@ -112,4 +112,39 @@ void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float sc
 void set_step(hipStream_t s, StepState* st, int kv_len, int position);
 void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uint16_t* dst);
 
+
+// ---- fused decode step (kernels_step.hip): batch 1, one launch per token
+struct DecodeStepDesc {
+    int layers;
+    const uint16_t* ln1[28];
+    const uint16_t* wqkv[28];
+    const uint16_t* wo[28];
+    const uint16_t* ln2[28];
+    const uint16_t* wgu[28];
+    const uint16_t* wdn[28];
+    uint16_t* kc[28];
+    uint16_t* vc[28];
+    const int64_t* ids;
+    const uint16_t* E;
+    const uint16_t* fnorm;
+    float normalizer, eps, scale;
+    long long pad_id;
+    const uint16_t *cosT, *sinT;
+    int max_pos;
+    const StepState* st;
+    uint16_t *h, *q, *act;
+    float* part;
+    int max_chunks;
+    long kvb;
+    int nh, nkv, H, I, V;
+    float* logits;
+    float* pmax;
+    int* pidx;
+    int64_t* next;
+    unsigned* sync;
+    unsigned* err;
+};
+int decode_step_sync_words(int layers);
+int decode_step_launch(hipStream_t s, const DecodeStepDesc& d);
+
 }  // namespace pgmi

@@ -59,6 +59,8 @@ SIGNATURES = {
     "pgmi_embed": (i32, [vp, vp, i32, vp, vp]),
     "pgmi_lm_forward": (i32, [vp, vp, vp, i32, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
     "pgmi_decode": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
+    "pgmi_set_decode_fused": (i32, [vp, i32]),
+    "pgmi_decode_status": (i32, [vp, vp]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),

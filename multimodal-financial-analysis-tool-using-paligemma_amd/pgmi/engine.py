@@ -232,6 +232,16 @@ class Engine:
                 "pgmi_decode")
         return logits
 
+    def set_decode_fused(self, on: bool) -> None:
+        """Batch-1 decode as one dataflow launch per token (default) or one launch per phase."""
+        N.check(self.lib.pgmi_set_decode_fused(self.ctx, int(bool(on))), "pgmi_set_decode_fused")
+
+    def decode_status(self) -> int:
+        """Sticky status of the fused decode step (bit 0: a phase wait timed out); cleared on read."""
+        st = ctypes.c_uint(0)
+        N.check(self.lib.pgmi_decode_status(self.ctx, ctypes.addressof(st)), "pgmi_decode_status")
+        return int(st.value)
+
     def argmax(self, logits: torch.Tensor) -> torch.Tensor:
         l2 = logits.reshape(-1, logits.shape[-1]).contiguous()
         out = torch.empty(l2.shape[0], dtype=torch.int64, device=self.device)

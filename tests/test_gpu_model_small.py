@@ -94,3 +94,49 @@ def test_batched_decode_matches_single(eng, gold):
     for i in range(3):
         t1 = eng.generate(ids[i:i + 1], pxs[i:i + 1], 6, graph=False).cpu().numpy()
         assert np.array_equal(tb[i], t1[0]), (i, tb[i], t1[0])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_step_matches_per_phase_launches(eng, gold, graph):
+    """The batch-1 decode step as one dataflow launch (kernels_step.hip) computes exactly what
+    the per-phase launches compute: bit-identical logits, KV rows and tokens, every step, with
+    no phase-wait timeout; also across a chunk boundary of the 64-key attention partials."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    L = ids.shape[1]
+    feats = eng.project(eng.vision(px))
+    kv_a = eng.new_kv(1, 1024)
+    eng.lm_forward(kv_a, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)
+    kv_b = kv_a.clone()
+    tok = torch.tensor([108], device="cuda")
+    n = 40  # L = 288: positions 288..327 cross the 320-key chunk boundary
+    try:
+        for t in range(n):
+            eng.set_decode_fused(True)
+            la = eng.decode(tok, kv_a, L + t, L + t + 1, graph=graph).clone()
+            eng.set_decode_fused(False)
+            lb = eng.decode(tok, kv_b, L + t, L + t + 1, graph=graph).clone()
+            torch.cuda.synchronize()
+            assert torch.equal(la, lb), (t, (la - lb).abs().max().item())
+            tok = la.argmax(-1)
+    finally:
+        eng.set_decode_fused(True)
+    assert eng.decode_status() == 0
+    assert torch.equal(kv_a, kv_b)
+
+
+def test_fused_step_next_ids(eng, gold):
+    """Device-side argmax of the fused step == torch.argmax of its logits."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    L = ids.shape[1]
+    kv = eng.new_kv(1, 1024)
+    eng.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=eng.project(eng.vision(px)), logits_rows=1)
+    nxt = torch.empty(1, dtype=torch.int64, device="cuda")
+    tok = torch.tensor([108], device="cuda")
+    for t in range(8):
+        lg = eng.decode(tok, kv, L + t, L + t + 1, next_ids=nxt, graph=True)
+        torch.cuda.synchronize()
+        assert int(nxt[0]) == int(lg.argmax(-1)[0])
+        tok = nxt.clone()
+    assert eng.decode_status() == 0

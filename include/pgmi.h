@@ -117,13 +117,17 @@ int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, 
  *   use_graph != 0 replays a captured hipGraph of the whole step. */
 int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                 int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
-/* Batch-1 decode-step implementation: 1 (default; env PGMI_DECODE_FUSED=0 turns it off) = the
- * whole step as one dataflow launch whose workgroup ranges run the phases in dependency order
- * (kernels_step.hip); 0 = one launch per phase.  Same arithmetic either way. */
+/* Batch-1 decode-step implementation: 0 (default) = one launch per phase, captured in a hipGraph;
+ * 1 (or env PGMI_DECODE_FUSED=1) = the whole step as one dataflow launch whose workgroup ranges
+ * run the phases in dependency order (kernels_step.hip).  Same arithmetic, bit-identical
+ * results; the per-phase launches are faster on MI355X today. */
 int pgmi_set_decode_fused(pgmi_ctx* ctx, int on);
 /* Sticky status of the fused step, cleared on read: bit 0 = a phase wait timed out (results of
  * that step are invalid). */
 int pgmi_decode_status(pgmi_ctx* ctx, unsigned* status);
+/* Diagnostics (env PGMI_STEP_TRACE=1): per-workgroup s_memrealtime stamps {entry, inputs ready,
+ * outputs published, -} of the last fused step, copied to host; returns workgroups copied. */
+int pgmi_decode_trace(pgmi_ctx* ctx, long long* host, long n_words);
 
 /* torch.argmax(logits, -1) over rows of a device fp32 [rows][V] matrix (inference.py:68) */
 int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* out, void* stream);

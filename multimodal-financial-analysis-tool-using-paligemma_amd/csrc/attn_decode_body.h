@@ -22,7 +22,8 @@ constexpr int DCH = 64;                 // keys per chunk
 constexpr int PSTRIDE = 16 * 256 + 32;  // per-chunk partial record: O_c[16][256], m_c[16], l_c[16]
 constexpr int DVS = 256 + 16;           // V row stride in LDS (elements): tr16 reads 2-way at most
 constexpr int DPS = DCH + 8;            // P row stride in LDS (elements)
-constexpr int kAttnDecodeLds = DCH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2 + 2 * 16 * 4;
+constexpr int DVH = DCH / 2;           // V rows staged in LDS at a time (two halves per chunk)
+constexpr int kAttnDecodeLds = DVH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2 + 2 * 16 * 4;
 
 typedef short s4v_t __attribute__((ext_vector_type(4)));
 
@@ -44,10 +45,10 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     if (chunk >= nch) return;  // (fused: no arrival; the consumer waits for nch chunks)
     const int t0 = chunk * DCH;
     const int nk = (Lk - t0) < DCH ? (Lk - t0) : DCH;
-    uint16_t* Vs = reinterpret_cast<uint16_t*>(lds);                          // [DCH][DVS]
-    float (*S)[DCH + 4] = reinterpret_cast<float (*)[DCH + 4]>(lds + DCH * DVS * 2);
-    uint16_t* Ps = reinterpret_cast<uint16_t*>(lds + DCH * DVS * 2 + 16 * (DCH + 4) * 4);
-    float (*stat)[16] = reinterpret_cast<float (*)[16]>(lds + DCH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2);
+    uint16_t* Vs = reinterpret_cast<uint16_t*>(lds);                          // [DVH][DVS]
+    float (*S)[DCH + 4] = reinterpret_cast<float (*)[DCH + 4]>(lds + DVH * DVS * 2);
+    uint16_t* Ps = reinterpret_cast<uint16_t*>(lds + DVH * DVS * 2 + 16 * (DCH + 4) * 4);
+    float (*stat)[16] = reinterpret_cast<float (*)[16]>(lds + DVH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2);
 
     // rows already in the cache before this step (F: the new row kv_len comes after the wait)
     const int n_old = F ? (kv_len - t0 < nk ? kv_len - t0 : nk) : nk;
@@ -92,11 +93,15 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
         for (int r = 0; r < 4; ++r)
             S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
     }
+    constexpr int VPH = DVH * 32 / 256;  // V chunks per thread per half
+    auto stage_v = [&](int half) {      // rows [32 half, 32 half + 32) of the chunk -> Vs
 #pragma unroll
-    for (int i = 0; i < DCH * 32 / 256; ++i) {
-        const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        *reinterpret_cast<uint4*>(Vs + r * DVS + 8 * c) = vr[i];
-    }
+        for (int i = 0; i < VPH; ++i) {
+            const int e = tid + 256 * i, r = e >> 5, c = e & 31;
+            *reinterpret_cast<uint4*>(Vs + r * DVS + 8 * c) = vr[half * VPH + i];
+        }
+    };
+    stage_v(0);
     __syncthreads();
     // ---- chunk-local max / exp / sum: wave w handles head rows 4w..4w+3, lane = key
 #pragma unroll
@@ -115,28 +120,37 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     float* pb = part + ((long)(b * a.n_kv + kvh) * max_chunks + chunk) * PSTRIDE;
     {
         const int g = lane >> 4, li = lane & 15;
-        short8 pa[2];
+        f32x4 acc[4];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) pa[kk] = *reinterpret_cast<const short8*>(Ps + li * DPS + 32 * kk + 8 * g);
+        for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int ct = wave * 4 + j;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int kk = 0; kk < 2; ++kk) {  // V half kk holds keys [32 kk, 32 kk + 32)
+            if (kk == 1) {
+                __syncthreads();  // every wave is done with half 0
+                stage_v(1);
+                __syncthreads();
+            }
+            const short8 pa = *reinterpret_cast<const short8*>(Ps + li * DPS + 32 * kk + 8 * g);
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                const uint16_t* vp = Vs + (32 * kk + 8 * g + (li >> 2)) * DVS + ct * 16 + 4 * (li & 3);
+            for (int j = 0; j < 4; ++j) {
+                const int ct = wave * 4 + j;
+                const uint16_t* vp = Vs + (8 * g + (li >> 2)) * DVS + ct * 16 + 4 * (li & 3);
                 const s4v_t lo =
                     __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v_t*)(vp));
                 const s4v_t hi =
                     __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v_t*)(vp + 4 * DVS));
                 const short8 vbf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                acc = mfma16(pa[kk], vbf, acc);
+                acc[j] = mfma16(pa, vbf, acc[j]);
             }
-            // C map: col d = ct*16 + (lane & 15), row h = (lane >> 4)*4 + r
+        }
+        // C map: col d = ct*16 + (lane & 15), row h = (lane >> 4)*4 + r
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ct = wave * 4 + j;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int h = (lane >> 4) * 4 + r;
-                if (h < a.G) stxf<F>(pb + h * 256 + ct * 16 + li, acc[r]);
+                if (h < a.G) stxf<F>(pb + h * 256 + ct * 16 + li, acc[j][r]);
             }
         }
     }

@@ -20,7 +20,12 @@ struct Dep {
     const unsigned* wait = nullptr;  // counter to wait on (nullptr: none)
     unsigned target = 0;             // ... until it reaches this value
     unsigned* arrive = nullptr;      // counter to add 1 to when the workgroup's outputs are out
+    // two-level arrival (many producers): add to arrive_shard; the workgroup completing its
+    // shard (shard_n arrivals) adds 1 to `arrive` -- one word sees few atomics
+    unsigned* arrive_shard = nullptr;
+    unsigned shard_n = 0;
     unsigned* err = nullptr;         // sticky error word (spin timeout)
+    long long* trace = nullptr;      // optional [4] timestamps of this workgroup: entry, ready, done
 };
 
 __device__ __forceinline__ uint4 ld16_coh(const void* p) {
@@ -103,7 +108,7 @@ __device__ __forceinline__ void dep_wait(const Dep& d) {
         if (threadIdx.x == 0) {
             unsigned spins = 0;
             while (__hip_atomic_load(d.wait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < d.target) {
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(4);
                 // give up on timeout, or at once when another workgroup already timed out
                 if (++spins > kSpinLimit ||
                     (d.err && (spins & 63) == 0 &&
@@ -113,6 +118,7 @@ __device__ __forceinline__ void dep_wait(const Dep& d) {
                 }
             }
         }
+        if (d.trace && threadIdx.x == 0) d.trace[1] = __builtin_amdgcn_s_memrealtime();
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler barrier: no load hoisting
     }
@@ -123,7 +129,12 @@ __device__ __forceinline__ void dep_arrive(const Dep& d) {
     if (d.arrive) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(d.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            if (!d.arrive_shard ||
+                __hip_atomic_fetch_add(d.arrive_shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == d.shard_n)
+                __hip_atomic_fetch_add(d.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d.trace) d.trace[2] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 

@@ -5,6 +5,7 @@
 //   vision   SiglipVisionTransformer.forward   modeling_siglip.py:236-244
 //   lm       GemmaModel/GemmaForCausalLM        modeling_gemma.py:357-427
 //   decode   one inference.py loop iteration    inference.py:56-78
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -100,7 +101,9 @@ struct pgmi_ctx {
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* step_sync = nullptr;  // fused decode step: phase counters (zeroed per launch)
     unsigned* step_err = nullptr;   // fused decode step: sticky status
-    bool fused = true;              // batch-1 decode as one dataflow launch (kernels_step.hip)
+    bool fused = false;             // batch-1 decode as one dataflow launch (kernels_step.hip; opt-in)
+    long long* step_trace = nullptr;  // PGMI_STEP_TRACE=1: per-workgroup timestamps of the last step
+    long step_trace_blocks = 0;
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
 };
@@ -268,7 +271,7 @@ int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
     if (c.max_batch < 1 || c.max_batch > 8) return fail(PGMI_E_ARG, "max_batch must be in [1, 8]");
     if (c.v_hidden > 4096) return fail(PGMI_E_ARG, "v_hidden too large for the LayerNorm kernel");
     auto* x = new pgmi_ctx();
-    if (const char* v = std::getenv("PGMI_DECODE_FUSED")) x->fused = std::strcmp(v, "0") != 0;
+    if (const char* v = std::getenv("PGMI_DECODE_FUSED")) x->fused = std::strcmp(v, "0") != 0;  // opt-in
     x->c = c;
     if (x->c.max_kv <= 0) x->c.max_kv = c.t_max_pos;
     x->device = device;
@@ -698,6 +701,15 @@ static int decode_fused(pgmi_ctx* x, hipStream_t s, const int64_t* ids, void* kv
     d.nh = NH; d.nkv = NKV; d.H = H; d.I = c.t_intermediate; d.V = c.t_vocab;
     d.logits = logits; d.pmax = x->pmax; d.pidx = x->pidx; d.next = next_ids ? next_ids : x->d_next;
     d.sync = x->step_sync; d.err = x->step_err;
+    if (const char* tv = std::getenv("PGMI_STEP_TRACE"); tv && std::strcmp(tv, "0") != 0) {
+        const long n = decode_step_grid(d);
+        if (n > x->step_trace_blocks) {
+            int rc;
+            if ((rc = dalloc_t(x, &x->step_trace, (size_t)n * 4))) return rc;
+            x->step_trace_blocks = n;
+        }
+        d.trace = x->step_trace;
+    }
     if (decode_step_launch(s, d)) return fail(PGMI_E_HIP, "fused decode step launch failed");
     return 0;
 }
@@ -712,6 +724,14 @@ int pgmi_set_decode_fused(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
     x->fused = on != 0;
     return 0;
+}
+
+int pgmi_decode_trace(pgmi_ctx* x, long long* host, long n_words) {
+    if (!x || !host) return fail(PGMI_E_ARG, "null argument");
+    if (!x->step_trace) return fail(PGMI_E_STATE, "no trace: set PGMI_STEP_TRACE=1 before the step");
+    const long n = std::min(n_words, x->step_trace_blocks * 4);
+    HIPCHK(hipMemcpy(host, x->step_trace, (size_t)n * sizeof(long long), hipMemcpyDeviceToHost));
+    return (int)(n / 4);
 }
 
 int pgmi_decode_status(pgmi_ctx* x, unsigned* status) {

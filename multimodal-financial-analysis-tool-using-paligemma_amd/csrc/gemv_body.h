@@ -30,6 +30,7 @@ struct GemvArgs {
     int n_units;
     int K;
     int nb;                  // valid batch rows (<= template B)
+    int upb;                 // > 0: workgroup w owns units [w*upb, (w+1)*upb) (fused step); 0: interleaved
     int I;                   // GeGLU: up rows offset; QKV: number of q heads
     // outputs
     uint16_t* out;           // RES: h in/out [nb][N]; GEGLU: act [nb][I]; QKV: q [nb][nh*256]
@@ -70,8 +71,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave % WK, grp = wave / WK;
-    const int stride = nblk * GPB * RPW;
-    int bb = blk * GPB * RPW;  // block-uniform loop base
+    // unit range of this workgroup: interleaved over the grid, or one contiguous slice
+    const int stride = a.upb > 0 ? GPB * RPW : nblk * GPB * RPW;
+    int bb = a.upb > 0 ? blk * a.upb : blk * GPB * RPW;  // block-uniform loop base
+    const int bend = a.upb > 0 ? (bb + a.upb < a.n_units ? bb + a.upb : a.n_units) : a.n_units;
     int ub = bb + grp * RPW;
     const int kofs = wk * KCW * 512 + 8 * lane;
 
@@ -86,7 +89,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
             int u = base + i;
-            if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate work, result discarded
+            if (u >= bend) u = bend - 1;  // clamp: duplicate work, result discarded
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
                 const uint16_t* rp = a.W + row_of(u, j) * K + kofs;
@@ -95,7 +98,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             }
         }
     };
-    if (ub < a.n_units) issue(ub);
+    if (ub < bend) issue(ub);
     if constexpr (F) dep_wait(dep);  // inputs of this phase are out (weights already in flight)
 
     uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
@@ -248,12 +251,12 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
     for (int b = 0; b < B; ++b) { best[b] = -INFINITY; besti[b] = 0x7fffffff; }
 
-    while (bb < a.n_units) {
+    while (bb < bend) {
         // epilogue operands of this group (residual h, RoPE cos/sin), queued behind its weights
         float pre[RPW][B][2];
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
-            const int u = ub + i < a.n_units ? ub + i : a.n_units - 1;
+            const int u = ub + i < bend ? ub + i : bend - 1;
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 const int bq = b < a.nb ? b : a.nb - 1;
@@ -288,7 +291,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         const int cur = ub;
         ub += stride;
         bb += stride;
-        if (ub < a.n_units) issue(ub);  // next group's stream starts before this group's epilogue
+        if (ub < bend) issue(ub);  // next group's stream starts before this group's epilogue
 
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
@@ -325,7 +328,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
             const int u = cur + i;
-            if (u >= a.n_units) break;
+            if (u >= bend) break;
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 if (b >= a.nb) break;

@@ -21,6 +21,17 @@
 namespace pgmi {
 
 constexpr int kStepMaxLayers = 28;
+constexpr int kCntStride = 32;  // words between counter words: each on its own 128-B line
+constexpr int kShards = 32;     // arrival shards per phase (+1 top word the consumers poll)
+// Streaming phases: one contiguous slice of units per workgroup, ~one workgroup per CU, rounds
+// of (4 waves x RPW) units with the next round's rows in flight; few consumers per hand-off
+// (each reads its whole input coherently).  RPW keeps the kernel at <= 128 VGPRs (4 per CU).
+constexpr int kGuRpw = 1, kDnRpw = 1, kLmRpw = 2;
+constexpr int kGuUpb = 64;   // gate/up pairs per workgroup  (16384 / 64 = 256 workgroups)
+constexpr int kDnUpb = 8;    // down rows per workgroup      (2048 / 8 = 256)
+constexpr int kOUpb = 32;    // o_proj rows per workgroup    (2048 / 32 = 64)
+constexpr int kLmUpb = 1008; // lm_head rows per workgroup   (257216 / 1008 -> 256)
+constexpr int kPhaseWords = (kShards + 1) * kCntStride;
 
 struct StepLayerW {
     const uint16_t *ln1, *wqkv, *wo, *ln2, *wgu, *wdn;
@@ -47,14 +58,29 @@ struct StepArgs {
     float* pmax;
     int* pidx;
     int64_t* next;
-    unsigned* sync;  // [0] embed, [1 + 5l + phase] per layer, [1 + 5 layers] lm_head; zero between launches
+    unsigned* sync;  // counter i at sync[i * kCntStride]: 0 embed, 1 + 5l + phase, 1 + 5 layers lm_head
+    long long* trace;  // optional per-workgroup timestamps [grid][4]
     unsigned* err;
     int n_qkv, n_attn, n_o, n_gu, n_dn, n_lm;
 };
 
-__global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
+// phase i: top word (polled by consumers) then kShards shard words
+__device__ __forceinline__ unsigned* cnt_at(const StepArgs& a, int i) { return a.sync + (long)i * kPhaseWords; }
+
+// producer r of n in phase i: shard r % kShards (holding ceil((n - s) / kShards) producers)
+__device__ __forceinline__ void set_arrive(Dep& d, const StepArgs& a, int i, int r, int n) {
+    const int sh = r % kShards;
+    d.arrive = cnt_at(a, i);
+    d.arrive_shard = cnt_at(a, i) + (1 + sh) * kCntStride;
+    d.shard_n = (unsigned)((n - sh + kShards - 1) / kShards);
+}
+// consumers of a phase with n producers wait for this many completed shards
+__host__ __device__ __forceinline__ unsigned shards_of(int n) { return (unsigned)(n < kShards ? n : kShards); }
+
+__global__ void __launch_bounds__(256, 4) k_decode_step(StepArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
     const int tid = threadIdx.x;
+    if (a.trace && tid == 0) a.trace[(long)blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
     const int per = a.n_qkv + a.n_attn + a.n_o + a.n_gu + a.n_dn;
     int bid = blockIdx.x;
     if (bid == 0) {  // embedding row x bf16(sqrt(H)) (modeling_gemma.py:367-369), pad id -> zeros
@@ -73,7 +99,8 @@ __global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
             st16_coh(a.h + c, *reinterpret_cast<const uint4*>(&o));
         }
         Dep d;
-        d.arrive = a.sync;
+        d.trace = a.trace ? a.trace + (long)blockIdx.x * 4 : nullptr;
+        set_arrive(d, a, 0, 0, 1);
         dep_arrive(d);
         return;
     }
@@ -82,13 +109,14 @@ __global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
         const int l = bid / per;
         int r = bid - l * per;
         const StepLayerW& w = a.L[l];
-        unsigned* cnt = a.sync + 1 + 5 * l;
+        const int c0 = 1 + 5 * l;  // this layer's phase counters c0 .. c0 + 4
         Dep d;
         d.err = a.err;
+        d.trace = a.trace ? a.trace + (long)blockIdx.x * 4 : nullptr;
         if (r < a.n_qkv) {
-            d.wait = l == 0 ? a.sync : cnt - 1;  // embed, or the previous layer's down phase
-            d.target = l == 0 ? 1u : (unsigned)a.n_dn;
-            d.arrive = cnt + 0;
+            d.wait = cnt_at(a, c0 - 1);  // embed, or the previous layer's down phase
+            d.target = shards_of(l == 0 ? 1 : a.n_dn);
+            set_arrive(d, a, c0, r, a.n_qkv);
             GemvArgs g{};
             g.x = a.h; g.norm_w = w.ln1; g.eps = a.eps; g.W = w.wqkv; g.n_units = (a.nh + 2 * a.nkv) * 128;
             g.K = a.H; g.nb = 1; g.I = a.nh; g.out = a.q; g.cosT = a.cosT; g.sinT = a.sinT; g.max_pos = a.max_pos;
@@ -98,9 +126,9 @@ __global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
         }
         r -= a.n_qkv;
         if (r < a.n_attn) {
-            d.wait = cnt + 0;
-            d.target = (unsigned)a.n_qkv;
-            d.arrive = cnt + 1;
+            d.wait = cnt_at(a, c0);
+            d.target = shards_of(a.n_qkv);
+            set_arrive(d, a, c0 + 1, r, (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk);
             const int kvd = a.nkv * 256;
             AttnArgs at{};
             at.q = a.q; at.q_b_stride = (long)a.nh * 256; at.q_row_stride = a.nh * 256; at.q_head_stride = 256;
@@ -112,54 +140,56 @@ __global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
         }
         r -= a.n_attn;
         if (r < a.n_o) {
-            d.wait = cnt + 1;
-            d.target = (unsigned)((a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk);
-            d.arrive = cnt + 2;
+            d.wait = cnt_at(a, c0 + 1);
+            d.target = shards_of((a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk);
+            set_arrive(d, a, c0 + 2, r, a.n_o);
             GemvArgs g{};
             g.W = w.wo; g.n_units = a.H; g.K = a.nh * 256; g.nb = 1; g.out = a.h; g.part = a.part;
-            g.max_chunks = a.max_chunks; g.G = a.nh / a.nkv; g.st = a.st;
+            g.max_chunks = a.max_chunks; g.G = a.nh / a.nkv; g.st = a.st; g.upb = kOUpb;
             gemv_block<1, 4, 2, GV_ORES, 1, false, true>(g, r, a.n_o, reinterpret_cast<uint16_t*>(lds), d);
             return;
         }
         r -= a.n_o;
         if (r < a.n_gu) {
-            d.wait = cnt + 2;
-            d.target = (unsigned)a.n_o;
-            d.arrive = cnt + 3;
+            d.wait = cnt_at(a, c0 + 2);
+            d.target = shards_of(a.n_o);
+            set_arrive(d, a, c0 + 3, r, a.n_gu);
             GemvArgs g{};
             g.x = a.h; g.norm_w = w.ln2; g.eps = a.eps; g.W = w.wgu; g.n_units = a.I; g.K = a.H; g.nb = 1;
-            g.I = a.I; g.out = a.act;
-            gemv_block<1, 4, 2, GV_GEGLU, 1, true, true>(g, r, a.n_gu, nullptr, d);
+            g.I = a.I; g.out = a.act; g.upb = kGuUpb;
+            gemv_block<1, 4, kGuRpw, GV_GEGLU, 1, true, true>(g, r, a.n_gu, nullptr, d);
             return;
         }
         r -= a.n_gu;
-        d.wait = cnt + 3;
-        d.target = (unsigned)a.n_gu;
-        d.arrive = cnt + 4;
+        d.wait = cnt_at(a, c0 + 3);
+        d.target = shards_of(a.n_gu);
+        set_arrive(d, a, c0 + 4, r, a.n_dn);
         GemvArgs g{};
-        g.x = a.act; g.W = w.wdn; g.n_units = a.H; g.K = a.I; g.nb = 1; g.out = a.h;
-        gemv_block<1, 32, 2, GV_RES, 4, true, true>(g, r, a.n_dn, nullptr, d);
+        g.x = a.act; g.W = w.wdn; g.n_units = a.H; g.K = a.I; g.nb = 1; g.out = a.h; g.upb = kDnUpb;
+        gemv_block<1, 32, kDnRpw, GV_RES, 4, true, true>(g, r, a.n_dn, nullptr, d);
         return;
     }
     bid -= a.layers * per;
-    unsigned* lm_cnt = a.sync + 1 + 5 * a.layers;
+    const int lm_c = 1 + 5 * a.layers;
     if (bid < a.n_lm) {  // final RMSNorm + tied lm_head, fp32 logits + per-workgroup first max
         Dep d;
         d.err = a.err;
-        d.wait = lm_cnt - 1;
-        d.target = (unsigned)a.n_dn;
-        d.arrive = lm_cnt;
+        d.trace = a.trace ? a.trace + (long)blockIdx.x * 4 : nullptr;
+        d.wait = cnt_at(a, lm_c - 1);
+        d.target = shards_of(a.n_dn);
+        set_arrive(d, a, lm_c, bid, a.n_lm);
         GemvArgs g{};
         g.x = a.h; g.norm_w = a.fnorm; g.eps = a.eps; g.W = a.E; g.n_units = a.V; g.K = a.H; g.nb = 1;
-        g.logits = a.logits; g.pmax = a.pmax; g.pidx = a.pidx;
-        gemv_block<1, 4, 4, GV_LOGITS, 1, true, true>(g, bid, a.n_lm, nullptr, d);
+        g.logits = a.logits; g.pmax = a.pmax; g.pidx = a.pidx; g.upb = kLmUpb;
+        gemv_block<1, 4, kLmRpw, GV_LOGITS, 1, true, true>(g, bid, a.n_lm, nullptr, d);
         return;
     }
     // argmax over the lm_head partials (torch.argmax: first maximum wins, inference.py:68)
     Dep d;
     d.err = a.err;
-    d.wait = lm_cnt;
-    d.target = (unsigned)a.n_lm;
+    d.trace = a.trace ? a.trace + (long)blockIdx.x * 4 : nullptr;
+    d.wait = cnt_at(a, lm_c);
+    d.target = shards_of(a.n_lm);
     dep_wait(d);
     float best = -INFINITY;
     int bi = 0x7fffffff;
@@ -185,12 +215,18 @@ __global__ void __launch_bounds__(256) k_decode_step(StepArgs a) {
     // Every other workgroup has passed its last wait (each arrived after waiting, and all
     // arrivals precede the lm_head count this workgroup waited for; attention workgroups past
     // the last chunk never wait): re-arm the counters for the next launch.
-    const int nw = 2 + 5 * a.layers;
-    for (int i = tid; i < nw; i += 256) __hip_atomic_store(a.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = tid; i < (lm_c + 1) * (kShards + 1); i += 256)
+        __hip_atomic_store(a.sync + (long)i * kCntStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- host side
-int decode_step_sync_words(int layers) { return (2 + 5 * layers + 3) & ~3; }  // 16-B multiple
+int decode_step_sync_words(int layers) { return (2 + 5 * layers) * kPhaseWords; }
+
+long decode_step_grid(const DecodeStepDesc& d) {
+    return 1 + (long)d.layers * ((d.nh + 2 * d.nkv) * 128 / 4 + d.max_chunks + (d.H + kOUpb - 1) / kOUpb +
+                                 (d.I + kGuUpb - 1) / kGuUpb + (d.H + kDnUpb - 1) / kDnUpb) +
+           (d.V + kLmUpb - 1) / kLmUpb + 1;
+}
 
 int decode_step_launch(hipStream_t s, const DecodeStepDesc& d) {
     if (d.layers > kStepMaxLayers) return -1;
@@ -203,13 +239,13 @@ int decode_step_launch(hipStream_t s, const DecodeStepDesc& d) {
     a.scale = d.scale; a.pad_id = d.pad_id; a.cosT = d.cosT; a.sinT = d.sinT; a.max_pos = d.max_pos; a.st = d.st;
     a.h = d.h; a.q = d.q; a.act = d.act; a.part = d.part; a.max_chunks = d.max_chunks; a.kvb = d.kvb; a.nh = d.nh;
     a.nkv = d.nkv; a.H = d.H; a.I = d.I; a.V = d.V; a.logits = d.logits; a.pmax = d.pmax; a.pidx = d.pidx;
-    a.next = d.next; a.sync = d.sync; a.err = d.err;
+    a.next = d.next; a.sync = d.sync; a.err = d.err; a.trace = d.trace;
     a.n_qkv = (d.nh + 2 * d.nkv) * 128 / 4;  // 4 row pairs per workgroup
     a.n_attn = d.max_chunks;
-    a.n_o = d.H / 8;                         // 8 rows per workgroup (4 waves x 2)
-    a.n_gu = d.I / 8;                        // 8 (gate, up) pairs per workgroup
-    a.n_dn = d.H / 2;                        // 2 rows per workgroup (K split over 4 waves)
-    a.n_lm = gemv_logits_blocks();
+    a.n_o = (d.H + kOUpb - 1) / kOUpb;
+    a.n_gu = (d.I + kGuUpb - 1) / kGuUpb;
+    a.n_dn = (d.H + kDnUpb - 1) / kDnUpb;
+    a.n_lm = (d.V + kLmUpb - 1) / kLmUpb;
     const long grid = 1 + (long)d.layers * (a.n_qkv + a.n_attn + a.n_o + a.n_gu + a.n_dn) + a.n_lm + 1;
     // counters start at zero (hipMemset at allocation) and the final workgroup re-arms them
     hipLaunchKernelGGL(k_decode_step, dim3((unsigned)grid), dim3(256), 0, s, a);

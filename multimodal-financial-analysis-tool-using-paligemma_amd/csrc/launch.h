@@ -143,8 +143,10 @@ struct DecodeStepDesc {
     int64_t* next;
     unsigned* sync;
     unsigned* err;
+    long long* trace;  // nullptr, or [grid][4] per-workgroup timestamps (diagnostics)
 };
 int decode_step_sync_words(int layers);
+long decode_step_grid(const DecodeStepDesc& d);
 int decode_step_launch(hipStream_t s, const DecodeStepDesc& d);
 
 }  // namespace pgmi

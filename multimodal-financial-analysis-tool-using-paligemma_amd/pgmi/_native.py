@@ -61,6 +61,7 @@ SIGNATURES = {
     "pgmi_decode": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
     "pgmi_set_decode_fused": (i32, [vp, i32]),
     "pgmi_decode_status": (i32, [vp, vp]),
+    "pgmi_decode_trace": (i32, [vp, vp, ctypes.c_long]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),

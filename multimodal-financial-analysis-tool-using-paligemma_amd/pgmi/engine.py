@@ -233,7 +233,7 @@ class Engine:
         return logits
 
     def set_decode_fused(self, on: bool) -> None:
-        """Batch-1 decode as one dataflow launch per token (default) or one launch per phase."""
+        """Batch-1 decode as one dataflow launch per token (opt-in) or one launch per phase (default)."""
         N.check(self.lib.pgmi_set_decode_fused(self.ctx, int(bool(on))), "pgmi_set_decode_fused")
 
     def decode_status(self) -> int:

@@ -120,7 +120,7 @@ def test_fused_step_matches_per_phase_launches(eng, gold, graph):
             assert torch.equal(la, lb), (t, (la - lb).abs().max().item())
             tok = la.argmax(-1)
     finally:
-        eng.set_decode_fused(True)
+        eng.set_decode_fused(False)
     assert eng.decode_status() == 0
     assert torch.equal(kv_a, kv_b)
 
@@ -134,9 +134,13 @@ def test_fused_step_next_ids(eng, gold):
     eng.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=eng.project(eng.vision(px)), logits_rows=1)
     nxt = torch.empty(1, dtype=torch.int64, device="cuda")
     tok = torch.tensor([108], device="cuda")
-    for t in range(8):
-        lg = eng.decode(tok, kv, L + t, L + t + 1, next_ids=nxt, graph=True)
-        torch.cuda.synchronize()
-        assert int(nxt[0]) == int(lg.argmax(-1)[0])
-        tok = nxt.clone()
+    eng.set_decode_fused(True)
+    try:
+        for t in range(8):
+            lg = eng.decode(tok, kv, L + t, L + t + 1, next_ids=nxt, graph=True)
+            torch.cuda.synchronize()
+            assert int(nxt[0]) == int(lg.argmax(-1)[0])
+            tok = nxt.clone()
+    finally:
+        eng.set_decode_fused(False)
     assert eng.decode_status() == 0

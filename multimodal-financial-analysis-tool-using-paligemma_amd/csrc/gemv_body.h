@@ -14,6 +14,8 @@
 //   - fp32 accumulation via v_dot2_f32_bf16, one wave reduction per output;
 //   - the reference's rounding points live in the epilogues (RoPE: modeling_gemma.py:
 //     197-198, KV append :259, residual :327/:336, GeGLU :134, logits :417-418).
+#include <type_traits>
+
 #include "coh.h"
 #include "common.h"
 #include "launch.h"
@@ -58,7 +60,7 @@ struct GemvArgs {
 // XREG: the activation lives in registers (lane's own K chunks), the RMSNorm is computed
 // per wave (WK == 1: every wave holds the whole row), no LDS staging / barrier; used when
 // B * K/(512*WK) chunks fit in 32 VGPRs.  Otherwise the activation is staged in LDS.
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, bool F>
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, bool F, int DEPTH = 1>
 __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, const int nblk, uint16_t* xs,
                                            const Dep& dep) {
     constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
@@ -84,8 +86,11 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         else return (long)u;
     };
 
-    uint4 w[NL];
-    auto issue = [&](int base) {
+    // DEPTH register sets of weight rows: groups g+1 .. g+DEPTH-1 stay in flight while group g
+    // is reduced (statically indexed: the loop below is unrolled by DEPTH)
+    uint4 w[DEPTH][NL];
+    auto issue = [&](auto slot, int base) {
+        constexpr int SL = decltype(slot)::value;
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
             int u = base + i;
@@ -94,11 +99,16 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             for (int j = 0; j < NR; ++j) {
                 const uint16_t* rp = a.W + row_of(u, j) * K + kofs;
 #pragma unroll
-                for (int c = 0; c < KCW; ++c) w[(i * NR + j) * KCW + c] = ldg_nt(rp + 512 * c);
+                for (int c = 0; c < KCW; ++c) w[SL][(i * NR + j) * KCW + c] = ldg_nt(rp + 512 * c);
             }
         }
     };
-    if (ub < bend) issue(ub);
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, DEPTH - 1>;
+    if (ub < bend) issue(S0{}, ub);
+    if constexpr (DEPTH == 2) {
+        if (ub + stride < bend) issue(S1{}, ub + stride);
+    }
     if constexpr (F) dep_wait(dep);  // inputs of this phase are out (weights already in flight)
 
     uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
@@ -251,7 +261,8 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
     for (int b = 0; b < B; ++b) { best[b] = -INFINITY; besti[b] = 0x7fffffff; }
 
-    while (bb < bend) {
+    auto step = [&](auto slot) {
+        constexpr int SL = decltype(slot)::value;
         // epilogue operands of this group (residual h, RoPE cos/sin), queued behind its weights
         float pre[RPW][B][2];
 #pragma unroll
@@ -285,13 +296,14 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
                 for (int i = 0; i < RPW; ++i)
 #pragma unroll
-                    for (int j = 0; j < NR; ++j) acc[i][j][b] = dot8(w[(i * NR + j) * KCW + c], xv, acc[i][j][b]);
+                    for (int j = 0; j < NR; ++j) acc[i][j][b] = dot8(w[SL][(i * NR + j) * KCW + c], xv, acc[i][j][b]);
             }
         }
         const int cur = ub;
         ub += stride;
         bb += stride;
-        if (ub < bend) issue(ub);  // next group's stream starts before this group's epilogue
+        // the stream of group +DEPTH starts before this group's epilogue, into the freed set
+        if (ub + (DEPTH - 1) * stride < bend) issue(slot, ub + (DEPTH - 1) * stride);
 
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
@@ -322,7 +334,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                         acc[i][j][b] = t;
                     }
             __syncthreads();
-            if (wk != 0) continue;  // slice 0 of each group writes
+            if (wk != 0) return;  // slice 0 of each group writes
         }
 
 #pragma unroll
@@ -373,6 +385,13 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                 }
             }
         }
+    };
+    while (bb < bend) {
+        step(S0{});
+        if constexpr (DEPTH == 2) {
+            if (bb >= bend) break;
+            step(S1{});
+        }
     }
 
     if constexpr (MODE == GV_LOGITS) {
@@ -400,10 +419,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     if constexpr (F) dep_arrive(dep);
 }
 
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG>
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH>
 __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [B][K]
-    gemv_block<B, KCH, RPW, MODE, WK, XREG, false>(a, blockIdx.x, gridDim.x, xs, Dep{});
+    gemv_block<B, KCH, RPW, MODE, WK, XREG, false, DEPTH>(a, blockIdx.x, gridDim.x, xs, Dep{});
 }
 
 }  // namespace pgmi

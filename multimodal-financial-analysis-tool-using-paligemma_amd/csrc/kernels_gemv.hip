@@ -1,22 +1,30 @@
 // kernels_gemv.hip -- launchers of the decode GEMV kernels (bodies: gemv_body.h).
 #include "gemv_body.h"
 
+#include <cstdlib>
+
 namespace pgmi {
 
-template <int B, int KCH, int RPW, int MODE, int WK = 1>
+// launch-shape overrides for measurement sweeps (tools/gemv_sweep.py)
+static int tune_variant(const char* env, int dflt) {
+    const char* v = std::getenv(env);
+    return v ? std::atoi(v) : dflt;
+}
+
+template <int B, int KCH, int RPW, int MODE, int WK = 1, int DEPTH = 1>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
     constexpr bool XREG = (MODE != GV_ORES) && B * (KCH / WK) <= 8;
     size_t lds = XREG ? 0 : (size_t)B * KCH * 512 * sizeof(uint16_t);
     static size_t attr = 0;  // largest dynamic LDS size granted so far
     if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
     constexpr int per_block = (4 / WK) * RPW;
     int blocks = (a.n_units + per_block - 1) / per_block;
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK, XREG>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH>), dim3(blocks), dim3(256), lds, s, a);
 }
 
 // K = 2048 (hidden); nh q heads, nkv kv heads of 256
@@ -28,7 +36,11 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
-    if (B <= 1) L_(1, 4, 1, GV_QKV);
+    if (B <= 1) {
+        const int cap = tune_variant("PGMI_QKV_CAP", 0);
+        if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
+        else launch_gemv<1, 4, 1, GV_QKV>(s, a, cap);
+    }
     else if (B <= 2) L_(2, 4, 1, GV_QKV);
     else if (B <= 4) L_(4, 4, 1, GV_QKV);
     else L_(8, 4, 1, GV_QKV);
@@ -47,7 +59,13 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
             const int nb = (B - b0) < 4 ? (B - b0) : 4;
             GemvArgs c = a;
             c.x = x + (long)b0 * K; c.out = h_inout + (long)b0 * N; c.nb = nb;
-            if (nb <= 1) launch_gemv<1, 32, 2, GV_RES, 4>(s, c, 512);
+            if (nb <= 1) {
+                const int cap = tune_variant("PGMI_DOWN_CAP", 512);
+                const int rpw = tune_variant("PGMI_DOWN_RPW", 1);
+                if (tune_variant("PGMI_DOWN_DEPTH", 1) == 2) launch_gemv<1, 32, 1, GV_RES, 4, 2>(s, c, cap);
+                else if (rpw == 1) launch_gemv<1, 32, 1, GV_RES, 4>(s, c, cap);
+                else launch_gemv<1, 32, 2, GV_RES, 4>(s, c, cap);
+            }
             else if (nb <= 2) launch_gemv<2, 32, 2, GV_RES, 4>(s, c);
             else launch_gemv<4, 32, 2, GV_RES, 4>(s, c);
         }
@@ -60,7 +78,11 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
     a.x = nullptr; a.norm_w = nullptr; a.W = Wo; a.n_units = N; a.K = G * 256; a.nb = B; a.out = h_inout;
     a.part = part; a.max_chunks = max_chunks; a.G = G; a.st = st; a.o_out = o_out;
     // grid capped so each workgroup's combine prologue is amortised over 8 output rows
-    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, 256);
+    if (B <= 1) {
+        const int cap = tune_variant("PGMI_O_CAP", 256);
+        if (tune_variant("PGMI_O_RPW", 2) == 1) launch_gemv<1, 4, 1, GV_ORES>(s, a, cap);
+        else launch_gemv<1, 4, 2, GV_ORES>(s, a, cap);
+    }
     else if (B <= 2) launch_gemv<2, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 4) launch_gemv<4, 4, 1, GV_ORES>(s, a, 256);
     else launch_gemv<8, 4, 1, GV_ORES>(s, a, 256);
@@ -70,7 +92,13 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
                 int I, uint16_t* act) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
-    if (B <= 1) launch_gemv<1, 4, 2, GV_GEGLU>(s, a, 1024);
+    if (B <= 1) {
+        const int cap = tune_variant("PGMI_GU_CAP", 1024);
+        const int rpw = tune_variant("PGMI_GU_RPW", 1);
+        if (tune_variant("PGMI_GU_DEPTH", 1) == 2) launch_gemv<1, 4, 1, GV_GEGLU, 1, 2>(s, a, cap);
+        else if (rpw == 1) launch_gemv<1, 4, 1, GV_GEGLU>(s, a, cap);
+        else launch_gemv<1, 4, 2, GV_GEGLU>(s, a, cap);
+    }
     else if (B <= 2) L_(2, 4, 2, GV_GEGLU);
     else if (B <= 4) L_(4, 4, 2, GV_GEGLU);
     else L_(8, 4, 1, GV_GEGLU);
@@ -83,7 +111,8 @@ void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
-    const int mb = gemv_logits_blocks();
+    int mb = tune_variant("PGMI_LM_CAP", gemv_logits_blocks());
+    if (mb < 1 || mb > gemv_logits_blocks()) mb = gemv_logits_blocks();  // pmax/pidx capacity
     int blocks;
 #define LG_(b_, rpw)                                                    \
     do {                                                                \
@@ -91,7 +120,17 @@ void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
         if (blocks > mb) blocks = mb;                                   \
         launch_gemv<b_, 4, rpw, GV_LOGITS>(s, a, mb);                   \
     } while (0)
-    if (B <= 1) LG_(1, 4);
+    if (B <= 1) {
+        if (tune_variant("PGMI_LM_DEPTH", 1) == 2) {
+            blocks = (V + 8 - 1) / 8;
+            if (blocks > mb) blocks = mb;
+            launch_gemv<1, 4, 2, GV_LOGITS, 1, 2>(s, a, mb);
+        } else if (tune_variant("PGMI_LM_RPW", 4) == 2) {
+            LG_(1, 2);
+        } else {
+            LG_(1, 4);
+        }
+    }
     else if (B <= 2) LG_(2, 4);
     else if (B <= 4) LG_(4, 2);
     else LG_(8, 2);

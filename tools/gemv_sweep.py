@@ -1,0 +1,46 @@
+"""Time the decode gate/up and down GEMVs (pgmi_decode_kernel 2 / 3, cycling the 18 layers so
+weights come from HBM) for the launch-shape variant selected by PGMI_GU_RPW/CAP /
+PGMI_DOWN_RPW/CAP.  Run once per variant (the variant is read per launch from the env)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multimodal-financial-analysis-tool-using-paligemma_amd"), REPO]
+import torch  # noqa: E402
+
+from oracle import weights as W  # noqa: E402
+from pgmi import Engine  # noqa: E402
+from pgmi import _native as N  # noqa: E402
+
+
+def timeit(e, which, iters=90):
+    s = torch.cuda.current_stream()
+    for i in range(18):
+        N.check(e.lib.pgmi_decode_kernel(e.ctx, which, i % 18, 1, s.cuda_stream))
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for i in range(iters):
+        N.check(e.lib.pgmi_decode_kernel(e.ctx, which, i % 18, 1, s.cuda_stream))
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / iters
+
+
+def main():
+    e = Engine(W.full_config(224), max_batch=1, max_seq=320, max_kv=512)
+    e.fill_synthetic(1234, W.init_policy)
+    e.prepare()
+    for rpw in (1, 2):
+        for cap in (256, 384, 512, 768, 1024):
+            os.environ["PGMI_GU_RPW"], os.environ["PGMI_GU_CAP"] = str(rpw), str(cap)
+            t = timeit(e, 2)
+            print(f"gate/up rpw {rpw} cap {cap:4d}: {t:6.2f} us  {134217728 / t / 1e3:6.0f} GB/s", flush=True)
+    for rpw in (1, 2):
+        for cap in (128, 256, 384, 512, 768):
+            os.environ["PGMI_DOWN_RPW"], os.environ["PGMI_DOWN_CAP"] = str(rpw), str(cap)
+            t = timeit(e, 3)
+            print(f"down rpw {rpw} cap {cap:4d}: {t:6.2f} us  {67108864 / t / 1e3:6.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -820,7 +820,7 @@ int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
 }
 
 int pgmi_tune_gemm(int cfg, int split) {
-    if (cfg > 5 || split < 0 || split > 16) return fail(PGMI_E_ARG, "bad GEMM plan");
+    if (cfg > 19 || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
     gemm_force_plan(cfg, split);
     return 0;
 }

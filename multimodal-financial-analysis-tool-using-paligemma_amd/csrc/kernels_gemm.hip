@@ -14,6 +14,8 @@
 #include "common.h"
 #include "launch.h"
 
+#include <cstdlib>
+
 namespace pgmi {
 
 constexpr int BK = 64;
@@ -187,6 +189,214 @@ __global__ void k_splitk_epi(const float* __restrict__ ws, int S, int M, int N, 
     }
 }
 
+// ---------------------------------------------------------------- panel GEMM (LDS-DMA ring)
+// One 256-thread workgroup (one wave per SIMD, 1 workgroup per CU) owns BM = 2*TM*16 rows x
+// BN = 2*TN*16 columns (per B operand; NB = 2 for the dual gate/up GEMM).  Both operands go
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows x 128 B per wave
+// instruction) into an ST-slot ring of 64-deep k-tiles; the loads of tile t+ST-1 are issued
+// right after the barrier that retires tile t and stay in flight across the next barriers
+// (counted vmcnt, raw s_barrier).  LDS rows are 128 B with the 16-B chunk index XOR-ed by
+// (row & 7): the swizzle is applied to each lane's SOURCE address (LDS-DMA destinations are
+// lane-linear), and the matching XOR on the ds_read_b128 fragment reads makes them
+// bank-conflict free.  K tails (K % 64, e.g. SigLIP fc2 K = 4304) read a zero block.
+// Waves form a 2 x 2 grid; wave (wm, wn) owns TM x TN (x NB) 16x16 MFMA tiles.
+__device__ __attribute__((aligned(16))) uint4 g_zero_chunk[1] = {{0u, 0u, 0u, 0u}};
+
+// s_waitcnt vmcnt(G * n) for a runtime n in [0, NMAX] (the count must be an immediate)
+template <int G, int NMAX>
+__device__ __forceinline__ void vm_wait_tiles(int n) {
+    if constexpr (NMAX >= 1) {
+        if (n >= NMAX) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * NMAX) : "memory");
+            return;
+        }
+        vm_wait_tiles<G, NMAX - 1>(n);
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+template <int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(256, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
+                                                   const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                   int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
+                                                   int n_mt, int n_nt, int krot) {
+    constexpr int WN = 4 / WM;
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
+    constexpr int PCS = APC + BPC;
+    static_assert(PCS % 4 == 0, "pieces must split evenly over 4 waves");
+    constexpr int GPW = PCS / 4;                    // LDS-DMA instructions per wave per k-tile
+    constexpr int ABYTES = BM * 128;
+    constexpr int SBYTES = (BM + NB * BN) * 128;    // one ring slot
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_p[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    // tile coordinates: the M tiles of one N tile share an XCD (blocks b, b+8, ... do), so a
+    // weight tile is fetched from HBM once per XCD rather than once per M tile
+    const int b = blockIdx.x;
+    int mt, nt;
+    if ((n_nt & 7) == 0) {
+        const int j = b >> 3;
+        mt = j % n_mt;
+        nt = (j / n_mt) * 8 + (b & 7);
+    } else {
+        mt = b % n_mt;
+        nt = b / n_mt;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int nkt_total = (K + 63) / 64;
+    const int kt0 = blockIdx.y * kt_per_split;
+    int kt1 = kt0 + kt_per_split;
+    if (kt1 > nkt_total) kt1 = nkt_total;
+    const int nkt = kt1 - kt0;
+    // k-tile order rotated per column tile: workgroups sharing A rows start at different k, so
+    // they do not all hit the same L2 lines (channels) at once
+    const int rot = nkt > 0 ? (nt * krot) % nkt : 0;
+
+    // per-lane source rows of this wave's pieces (piece p = wave + 4 i)
+    const uint16_t* src[GPW];
+    int gk[GPW];  // element offset of the lane's chunk inside a 64-wide k-tile
+    const int prow = lane >> 3;
+    const int pchunk = lane & 7;
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+        const int p = wave + 4 * i;
+        int row;
+        const uint16_t* base;
+        long ld;
+        if (p < APC) {
+            row = m0 + p * 8 + prow;
+            if (row > M - 1) row = M - 1;  // rows past M: valid memory, results never stored
+            base = A;
+            ld = lda;
+        } else {
+            const int q = p - APC;
+            const int bo = q / (BN / 8);
+            row = n0 + (q % (BN / 8)) * 8 + prow;
+            if (row > N - 1) row = N - 1;
+            base = W + bo * up_off;
+            ld = ldw;
+        }
+        // lane (row r, LDS chunk c) fetches global chunk c ^ (r & 7)
+        gk[i] = (pchunk ^ (row & 7)) * 8;
+        src[i] = base + (long)row * ld + gk[i];
+    }
+    // slot image is piece-linear: A pieces first, then B pieces (piece p at p KiB)
+#define PGMI_LDS_AT(slot, i) ((__attribute__((address_space(3))) void*)(smem_p + (slot) * SBYTES + (wave + 4 * (i)) * 1024))
+    const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+    auto issue = [&](int kt, int slot) {
+        kt += rot;
+        if (kt >= kt1) kt -= nkt;
+        const int kel = kt * 64;
+        if (kel + 64 <= K) {
+#pragma unroll
+            for (int i = 0; i < GPW; ++i)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel), PGMI_LDS_AT(slot, i), 16, 0, 0);
+        } else {  // K tail: chunks at or past K read zeros (K % 8 == 0)
+#pragma unroll
+            for (int i = 0; i < GPW; ++i) {
+                const uint16_t* g = (kel + gk[i] < K) ? src[i] + kel : zero;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), PGMI_LDS_AT(slot, i), 16, 0, 0);
+            }
+        }
+    };
+
+    f32x4 acc[NB][TM][TN];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[bb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int swz = lane & 7;  // fragment rows are 16-aligned + (lane & 15): row & 7 == lane & 7
+    const int arow0 = (wm * TM * 16 + (lane & 15)) * 128;
+    const int brow0 = ABYTES + (wn * TN * 16 + (lane & 15)) * 128;
+    // fragments of one 32-deep k step (kk = 0, 1 of a 64-deep tile), two register sets
+    short8 fa0[TM], fb0[NB][TN], fa1[TM], fb1[NB][TN];
+#define PGMI_SB() __builtin_amdgcn_sched_barrier(0)
+#define PGMI_READ_FRAGS(FA, FB, SLOT, KK)                                                                   \
+    do {                                                                                                    \
+        const uint8_t* sb_ = smem_p + (SLOT) * SBYTES;                                                      \
+        const int ch_ = ((((KK) * 4) + (lane >> 4)) ^ swz) << 4;                                            \
+        _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) FA[i_] =                                          \
+            *reinterpret_cast<const short8*>(sb_ + arow0 + i_ * 16 * 128 + ch_);                            \
+        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
+            FB[b_][j_] = *reinterpret_cast<const short8*>(sb_ + brow0 + (b_ * BN + j_ * 16) * 128 + ch_);   \
+    } while (0)
+#define PGMI_MFMAS(FA, FB)                                                                                  \
+    do {                                                                                                    \
+        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) \
+            _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) acc[b_][i_][j_] =                              \
+                mfma16(FA[i_], FB[b_][j_], acc[b_][i_][j_]);                                                \
+    } while (0)
+
+    // ring: tiles t+1 .. t+ST-1 in flight or landed while tile t is multiplied.  Per tile:
+    //   read kk=1 fragments | MFMAs kk=0 | retire tile t+1, barrier, refill the slot tile t
+    //   lived in with tile t+ST | read tile t+1's kk=0 fragments | MFMAs kk=1
+    // so every fragment read is covered by a block of MFMAs and the LDS-DMA of a tile has
+    // ST-1 tiles of MFMAs to land.
+#pragma unroll
+    for (int sI = 0; sI < ST; ++sI)
+        if (sI < nkt) issue(kt0 + sI, sI);
+    if (nkt > 0) {
+        vm_wait_tiles<GPW, ST - 1>((nkt < ST ? nkt : ST) - 1);
+        __builtin_amdgcn_s_barrier();
+        PGMI_READ_FRAGS(fa0, fb0, 0, 0);
+    }
+    int slot = 0;
+    for (int t = 0; t < nkt; ++t) {
+        // the kk=0 fragments (read behind the previous MFMA block) have landed; a real s_waitcnt
+        // (not asm) so the compiler's counter model knows nothing older is outstanding and does
+        // not drain the kk=1 reads below before the first MFMA
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        PGMI_READ_FRAGS(fa1, fb1, slot, 1);
+        PGMI_SB();
+        PGMI_MFMAS(fa0, fb0);
+        PGMI_SB();
+        if (t + 1 < nkt) {
+            // tiles issued so far: min(nkt, t + ST); tile t+1 must have landed
+            const int ahead = (nkt - t - 2) < (ST - 2) ? (nkt - t - 2) : (ST - 2);
+            vm_wait_tiles<GPW, ST - 2>(ahead);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): kk=1 reads done before the slot is refilled
+        __builtin_amdgcn_s_barrier();
+        PGMI_SB();
+        if (t + ST < nkt) issue(kt0 + t + ST, slot);
+        const int nslot = slot + 1 == ST ? 0 : slot + 1;
+        if (t + 1 < nkt) PGMI_READ_FRAGS(fa0, fb0, nslot, 0);
+        PGMI_SB();
+        PGMI_MFMAS(fa1, fb1);
+        PGMI_SB();
+        slot = nslot;
+    }
+#undef PGMI_READ_FRAGS
+#undef PGMI_MFMAS
+#undef PGMI_SB
+
+    // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
+                if (m < M && n < N) {
+                    if constexpr (SPLIT) {
+                        ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
+                    } else {
+                        epi_store<EPI>(ea, m, n, acc[0][i][j][r], NB == 2 ? acc[NB - 1][i][j][r] : 0.f);
+                    }
+                }
+            }
+        }
+}
+
 // Tile configurations (wave grid, per-wave MFMA tiles).  BM = WGM*TM*16, BN = WGN*TN*16.
 enum Cfg : int {
     C288x64 = 0,   // 6x1 waves, 3x4 tiles  (text rows: M = 288 = 18 x 16)
@@ -195,6 +405,22 @@ enum Cfg : int {
     C256x32 = 3,   // 4x1 waves, 4x2 tiles
     C128x128 = 4,  // 2x2 waves, 4x4 tiles  (large M)
     C128x64 = 5,   // 2x2 waves, 4x2 tiles
+    // panel GEMM (k_gemm_p, LDS-DMA ring): BM x BN output columns (dual gate/up: BN/2 columns x 2)
+    P288w = 6,     // TM 9,  BN 128, 3 slots
+    P256w = 7,     // TM 8,  BN 128, 3 slots
+    P352w = 8,     // TM 11, BN 128, 2 slots  (448 px text rows: M = 1056 = 3 x 352)
+    P288n = 9,     // TM 9,  BN 64,  3 slots
+    P256n = 10,    // TM 8,  BN 64,  3 slots
+    P128w = 11,    // TM 4,  BN 128, 3 slots
+    P288t = 12,    // TM 9,  BN 32,  4 slots  (2x2 waves, 1 column fragment each)
+    P256t = 13,    // 4x1 waves, TM 4, BN 32, 4 slots
+    P64x64 = 14,   // TM 2, BN 64,  6 slots   (small GEMMs: every CU busy, little A per CU)
+    P128x64 = 15,  // TM 4, BN 64,  6 slots
+    P64x128 = 16,  // TM 2, BN 128, 6 slots
+    P128x128 = 17, // TM 4, BN 128, 5 slots
+    P64x64d = 18,  // TM 2, BN 64,  10 slots
+    P128x64d = 19, // 4x1 waves, TM 2, BN 64, 6 slots
+    kNumCfg = 20,
 };
 
 struct Plan {
@@ -203,6 +429,10 @@ struct Plan {
 };
 
 static int g_force_cfg = -1, g_force_split = 0;  // tuning override (pgmi_tune_gemm)
+static int g_krot = [] {  // panel GEMM k-order rotation per column tile (PGMI_GEMM_KROT; 0 = off)
+    const char* v = std::getenv("PGMI_GEMM_KROT");
+    return v ? std::atoi(v) : 0;
+}();
 
 void gemm_force_plan(int cfg, int split) {
     g_force_cfg = cfg;
@@ -211,29 +441,50 @@ void gemm_force_plan(int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128}, bns[] = {64, 32, 64, 32, 128, 64};
-        return {(Cfg)g_force_cfg, bms[g_force_cfg], bns[g_force_cfg], dual ? 1 : (g_force_split > 0 ? g_force_split : 1)};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64};
+        const int c = g_force_cfg;
+        const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
+        return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
     }
-    // Measured on MI355X (tools/gemm_sweep.py, prefill shapes M = 256 / 288): the 2x2-wave
-    // 128x64 tile with split-K wins for the projection GEMMs; the 288-row panel (weights read
-    // once, A re-read from L2) wins for the dual gate/up GEMM and the K = 16384 down projection.
-    const int nkt = (K + BK - 1) / BK;
-    Plan p;
-    const bool small_m = M <= 288;
-    if (small_m && dual) {
-        p = {M <= 256 ? C256x64 : C288x64, M <= 256 ? 256 : 288, 64, 1};
-    } else if (small_m && K >= 8192) {
-        p = {M <= 256 ? C256x64 : C288x64, M <= 256 ? 256 : 288, 64, 1};
-    } else if (dual) {
-        p = {C128x128, 128, 128, 1};
-        return p;
-    } else {
-        p = {C128x64, 128, 64, 1};
-        if (!small_m && (long)((M + 127) / 128) * ((N + 127) / 128) >= 256) p = {C128x128, 128, 128, 1};
-    }
-    if (dual) return p;
-    const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
-    while (tiles * p.split < 200 && p.split < 8 && nkt / (p.split * 2) >= 2) p.split *= 2;
+    // Measured on MI355X (tools/gemm_sweep.py; GPU time of graph-replayed calls, round 1): the
+    // PaliGemma prefill shapes at 224 px (M = 256 vision / 288 text rows) and 448 px (1024 /
+    // 1056 rows).  Small GEMMs want every CU busy with little A per CU (64 x 64 tiles, 6-slot
+    // ring, no split: the epilogue stays in the GEMM); the dual gate/up and K = 16384 down
+    // projections want full-M panels that read each weight byte once.
+    struct Entry { int M, N, K; bool dual; Cfg cfg; int split; };
+    static const Entry table[] = {
+        {288, 2560, 2048, false, P64x64, 1},    // text q|k|v            11.5 us
+        {288, 2048, 2048, false, P64x64, 1},    // text o_proj           13.0 us
+        {288, 16384, 2048, true, P288w, 1},     // text gate|up (GeGLU)  50 us
+        {288, 2048, 16384, false, P288n, 8},    // text down             38 us
+        {256, 3456, 1152, false, P64x64, 1},    // vision q|k|v          10.1 us
+        {256, 1152, 1152, false, P64x64, 1},    // vision out_proj        9.9 us
+        {256, 4304, 1152, false, P128w, 3},     // vision fc1            18.5 us
+        {256, 1152, 4304, false, P64x64, 3},    // vision fc2            15.0 us
+        {256, 1152, 640, false, P64x64, 1},     // patch embedding        7.5 us
+        {256, 2048, 1152, false, P64x64, 1},    // multimodal projector   9.5 us
+        {1056, 2560, 2048, false, P128w, 1},    // 448 px text q|k|v     23.7 us
+        {1056, 2048, 2048, false, P288n, 2},    // 448 px text o_proj    28.2 us
+        {1056, 16384, 2048, true, P352w, 1},    // 448 px gate|up       165 us
+        {1056, 2048, 16384, false, P288w, 4},   // 448 px down           93 us
+        {1024, 4304, 1152, false, P352w, 2},    // 448 px vision fc1     37.6 us
+        {1024, 3456, 1152, false, P128w, 1},    // 448 px vision q|k|v   23.3 us
+    };
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64};
+    auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
+    for (const Entry& e : table)
+        if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
+    // other shapes (batched prefill: M = B x 256 / 288 rows; other image sizes)
+    if (dual) return mk(M <= 256 ? P256w : M <= 288 ? P288w : P352w, 1);
+    if (K >= 8192) return mk(M <= 288 ? P288n : P288w, M <= 288 ? 8 : 4);
+    const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (t64 <= 256) return mk(P64x64, 1);
+    const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+    Plan p = mk(P128w, 1);
+    const int nkt = (K + 63) / 64;
+    while (t128 * p.split < 200 && p.split < 4 && nkt / (p.split * 2) >= 4) p.split *= 2;
     return p;
 }
 
@@ -277,6 +528,72 @@ static void launch_t(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
 }
 
+#undef PGMI_LDS_AT
+
+// panel GEMM launcher: WM x (4/WM) waves, TNW = 16-column fragments per wave (per B operand
+// for plain GEMMs; the dual GEMM splits them over gate and up); EPI < 0: partials only
+template <int WM, int TM, int TNW, int ST, int EPI>
+static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                     const EpiArgs& ea, float* ws, int split, long up_off) {
+    constexpr bool DUAL = (EPI == EPI_GEGLU);
+    constexpr int NB = DUAL ? 2 : 1;
+    constexpr int TN = DUAL ? (TNW >= 2 ? TNW / 2 : 1) : TNW;  // the dual GEMM keeps the B rows per slot
+    constexpr int BM = WM * TM * 16, BN = (4 / WM) * TN * 16;
+    constexpr int STQ = (size_t)ST * (BM + NB * BN) * 128 <= 163840 ? ST : ST - 1;  // fit 160 KiB
+    constexpr size_t lds = (size_t)STQ * (BM + NB * BN) * 128;
+    static_assert(lds <= 163840, "LDS ring exceeds 160 KiB");
+    constexpr int EK = EPI < 0 ? EPI_STORE : EPI;
+    const int nkt = (K + 63) / 64;
+    const int per = (nkt + split - 1) / split;
+    const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
+    dim3 grid(n_mt * n_nt, split);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<WM, TM, TN, NB, STQ, EK, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<WM, TM, TN, NB, STQ, EK, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    if (EPI < 0 || split > 1) {
+        hipLaunchKernelGGL((k_gemm_p<WM, TM, TN, NB, STQ, EK, true>), grid, dim3(256), lds, s, A, lda, W, ldw, M, N, K, per,
+                           ea, ws, up_off, n_mt, n_nt, g_krot);
+        if (EPI >= 0) {
+            long total4 = ((long)M * N + 3) / 4;
+            long blocks = (total4 + 255) / 256;
+            if (blocks > 4096) blocks = 4096;
+            hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
+        }
+    } else {
+        hipLaunchKernelGGL((k_gemm_p<WM, TM, TN, NB, STQ, EK, false>), grid, dim3(256), lds, s, A, lda, W, ldw, M, N, K,
+                           per, ea, ws, up_off, n_mt, n_nt, g_krot);
+    }
+}
+
+template <int EPI>
+static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                        const EpiArgs& ea, float* ws, const Plan& p, long up_off) {
+#define P_(wm, tm, tn, st) launch_p<wm, tm, tn, st, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off)
+    switch (p.cfg) {
+        case P288w: P_(2, 9, 4, 3); break;
+        case P256w: P_(2, 8, 4, 3); break;
+        case P352w: P_(2, 11, 4, 2); break;
+        case P288n: P_(2, 9, 2, 3); break;
+        case P256n: P_(2, 8, 2, 4); break;
+        case P128w: P_(2, 4, 4, 3); break;
+        case P288t: P_(2, 9, 1, 4); break;
+        case P256t: P_(4, 4, 2, 4); break;
+        case P64x64: P_(2, 2, 2, 6); break;
+        case P128x64: P_(2, 4, 2, 6); break;
+        case P64x128: P_(2, 2, 4, 6); break;
+        case P128x128: P_(2, 4, 4, 5); break;
+        case P64x64d: P_(2, 2, 2, 10); break;
+        case P128x64d: P_(4, 2, 4, 6); break;
+        default: break;
+    }
+#undef P_
+}
+
 template <int EPI>
 static void launch_e(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                      const EpiArgs& ea, float* ws, const Plan& p, long up_off) {
@@ -287,6 +604,7 @@ static void launch_e(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         case C256x32: launch_t<4, 1, 4, 2, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case C128x128: launch_t<2, 2, 4, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case C128x64: launch_t<2, 2, 4, 2, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        default: launch_pcfg<EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
     }
 }
 
@@ -305,6 +623,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
             case C256x32: launch_t<4, 1, 4, 2, -1>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
             case C128x128: launch_t<2, 2, 4, 4, -1>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
             case C128x64: launch_t<2, 2, 4, 2, -1>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+            default: launch_pcfg<-1>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
         }
         return p.split;
     }

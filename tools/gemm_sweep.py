@@ -1,5 +1,8 @@
 """Sweep prefill GEMM plans (tile config x split-K) on the PaliGemma prefill shapes; prints
-us per call for each.  Usage (GPU box): python tools/gemm_sweep.py"""
+us per call, TFLOP/s and the max deviation from the reference plan (cfg 4/5 register-staged
+GEMM, checked by tests/test_gpu_ops.py).  Usage (GPU box):
+    python tools/gemm_sweep.py [shape-name ...] [--cfgs 6,7,9] [--splits 1,2,4,8]"""
+import argparse
 import os
 import sys
 
@@ -15,42 +18,82 @@ SHAPES = {  # name: (M, N, K, epi)
     "t_qkv": (288, 2560, 2048, 0), "t_o": (288, 2048, 2048, 4), "t_gateup": (288, 16384, 2048, 7),
     "t_down": (288, 2048, 16384, 4), "v_qkv": (256, 3456, 1152, 1), "v_out": (256, 1152, 1152, 3),
     "v_fc1": (256, 4304, 1152, 2), "v_fc2": (256, 1152, 4304, 3), "v_patch": (256, 1152, 640, 1),
+    "v_proj": (256, 2048, 1152, 1),
+    "t448_qkv": (1056, 2560, 2048, 0), "t448_o": (1056, 2048, 2048, 4), "t448_gateup": (1056, 16384, 2048, 7),
+    "t448_down": (1056, 2048, 16384, 4), "v448_fc1": (1024, 4304, 1152, 2), "v448_qkv": (1024, 3456, 1152, 1),
 }
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("shapes", nargs="*")
+    ap.add_argument("--cfgs", default="0,2,4,5,6,7,8,9,10,11")
+    ap.add_argument("--splits", default="1,2,4,8")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
     e = Engine(W.small_config(1, 1, 1024), max_batch=1, max_seq=320, max_kv=512)
     e.fill_synthetic(1, W.init_policy)
     e.prepare()
     lib = e.lib
     s = torch.cuda.current_stream().cuda_stream
-    for name, (M, Nn, K, epi) in SHAPES.items():
-        A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        Wt = (torch.randn(Nn * (2 if epi == 7 else 1), K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    cfgs = [int(c) for c in args.cfgs.split(",")]
+    splits = [int(c) for c in args.splits.split(",")]
+    torch.manual_seed(0)
+    for name in (args.shapes or SHAPES):
+        M, Nn, K, epi = SHAPES[name]
+        A = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        Wt = ((torch.rand(Nn * (2 if epi == 7 else 1), K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         bias = torch.randn(Nn, device="cuda").to(torch.bfloat16)
         res = torch.randn(M, Nn, device="cuda").to(torch.bfloat16)
         out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
-        res_line = []
-        for cfg, split in [(-1, 0)] + [(c, sp) for c in range(6) for sp in (1, 2, 4, 8)]:
-            if epi == 7 and split > 1:
-                continue
-            N.check(lib.pgmi_tune_gemm(cfg, split))
-            f = lambda: N.check(lib.pgmi_op_gemm(e.ctx, A.data_ptr(), Wt.data_ptr(), M, Nn, K, epi, bias.data_ptr(),  # noqa: E731
-                                                 res.data_ptr(), out.data_ptr(), s))
-            for _ in range(3):
-                f()
-            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            t0.record()
-            for _ in range(20):
-                f()
-            t1.record()
-            t1.synchronize()
-            res_line.append((t0.elapsed_time(t1) * 1e3 / 20, cfg, split))
+        flops = 2.0 * M * Nn * K * (2 if epi == 7 else 1)
+
+        def run(st=None):
+            N.check(lib.pgmi_op_gemm(e.ctx, A.data_ptr(), Wt.data_ptr(), M, Nn, K, epi, bias.data_ptr(),
+                                     res.data_ptr(), out.data_ptr(), st or s))
+
+        N.check(lib.pgmi_tune_gemm(4 if M > 288 else 5, 1))
+        run()
+        ref = out.float().clone()
+        rows = []
+        for cfg in [-1] + cfgs:
+            for split in ([0] if cfg < 0 else splits):
+                if epi == 7 and split > 1:
+                    continue
+                N.check(lib.pgmi_tune_gemm(cfg, split))
+                out.zero_()
+                run()
+                torch.cuda.synchronize()
+                err = float((out.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6))
+                for _ in range(3):
+                    run()
+                torch.cuda.synchronize()
+                # GPU time only: the calls are replayed from a captured graph (host launch cost,
+                # ~10 us through ctypes, would otherwise floor every small GEMM)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    cs = torch.cuda.current_stream().cuda_stream
+                    for _ in range(args.iters):
+                        run(cs)
+                g.replay()
+                torch.cuda.synchronize()
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                g.replay()
+                t1.record()
+                t1.synchronize()
+                us = t0.elapsed_time(t1) * 1e3 / args.iters
+                del g
+                rows.append((us, cfg, split, err))
         N.check(lib.pgmi_tune_gemm(-1, 0))
-        auto = res_line[0][0]
-        best = sorted(res_line[1:])[:4]
-        print(f"{name:9s} M={M} N={Nn} K={K}: auto {auto:7.1f} us | best " +
-              ", ".join(f"cfg{c}/s{sp}: {t:6.1f}" for t, c, sp in best), flush=True)
+        auto = rows[0]
+        best = sorted(rows[1:])[:5]
+        print(f"{name:12s} M={M} N={Nn} K={K}: auto {auto[0]:7.1f} us ({flops / auto[0] / 1e6:6.0f} TF) | " +
+              ", ".join(f"c{c}/s{sp}: {t:6.1f} ({flops / t / 1e6:4.0f} TF, err {er:.1e})" for t, c, sp, er in best),
+              flush=True)
+        bad = [(c, sp, er) for _, c, sp, er in rows if er > 2e-2]
+        if bad:
+            print(f"   MISMATCH {name}: {bad}", flush=True)
 
 
 if __name__ == "__main__":

@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-448", action="store_true", help="skip the 448 px prefill measurement (configs[4])")
     return ap.parse_args()
 
 
@@ -83,6 +84,66 @@ def cpu_baseline(cfg, seed, L, steps):
             "sample": f"{steps} KV-cached greedy decode steps of oracle/paligemma_np.py (numpy fp32 with bf16 "
                       f"rounding points) at full PaliGemma-3B text shapes, batch 1, cache {L} tokens; "
                       f"weight generation ({gen_s:.0f}s) untimed"}
+
+
+MFMA_BF16_PEAK_TFS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def time_prefill(eng, px, ids, pos, kv, iters):
+    """Median wall time (HIP events on the current stream) of pixels + ids -> last-row logits ->
+    argmax, with its vision / language-model split."""
+    import torch
+
+    def prefill():
+        feats = eng.project(eng.vision(px))
+        lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
+        return eng.argmax(lg[:, 0]), lg
+
+    for _ in range(3):
+        prefill()
+    torch.cuda.synchronize()
+    pre = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        prefill()
+        e1.record()
+        e1.synchronize()
+        pre.append(e0.elapsed_time(e1))
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record()
+    feats = eng.project(eng.vision(px))
+    e1.record()
+    lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
+    e2.record()
+    e2.synchronize()
+    return statistics.median(pre), e0.elapsed_time(e1), e1.elapsed_time(e2), lg
+
+
+def gemm_roofline(eng, rows, iters=36):
+    """The prefill's dominant MFMA GEMMs (gate|up + GeGLU, down) of all 18 layers over `rows`
+    token rows, timed with HIP events on the stream they are launched on."""
+    import torch
+    from pgmi import _native as N
+    t = eng.cfgd
+    H, I, nl = t["t_hidden"], t["t_intermediate"], t["t_layers"]
+    s = torch.cuda.current_stream()
+    out = {}
+    for which, name, flops in ((0, "gate_up_geglu", 2.0 * rows * 2 * I * H), (1, "down", 2.0 * rows * H * I)):
+        for i in range(nl):
+            N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i, rows, s.cuda_stream))
+        k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k0.record(s)
+        for i in range(iters):
+            N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i % nl, rows, s.cuda_stream))
+        k1.record(s)
+        k1.synchronize()
+        us = k0.elapsed_time(k1) * 1e3 / iters
+        tfs = flops / (us * 1e-6) / 1e12
+        out[name] = {"bound": "mfma", "rows": rows, "flop_per_launch": int(flops), "avg_launch_us": round(us, 2),
+                     "achieved": round(tfs, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(tfs / MFMA_BF16_PEAK_TFS, 4)}
+    return out
 
 
 def main():
@@ -130,32 +191,8 @@ def main():
     pos = torch.arange(L).expand(B, L)
     kv = eng.new_kv(B, kv_cap)
 
-    def prefill():
-        feats = eng.project(eng.vision(px))
-        lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
-        return eng.argmax(lg[:, 0])
-
-    for _ in range(3):
-        prefill()
-    torch.cuda.synchronize()
-    pre = []
-    for _ in range(a.prefill_iters):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        prefill()
-        e1.record()
-        e1.synchronize()
-        pre.append(e0.elapsed_time(e1))
-    prefill_ms = statistics.median(pre)
-    # split: vision tower + projector vs language model
-    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    e0.record()
-    feats = eng.project(eng.vision(px))
-    e1.record()
-    lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
-    e2.record()
-    e2.synchronize()
-    vision_ms, lm_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
+    prefill_ms, vision_ms, lm_ms, lg = time_prefill(eng, px, ids, pos, kv, a.prefill_iters)
+    prefill_gemms = gemm_roofline(eng, B * L)
 
     # ---- decode: warmup, then exactly K timed steps (graph replay, device-side argmax)
     first = eng.argmax(lg[:, 0])
@@ -216,6 +253,25 @@ def main():
         except Exception:
             traffic = None
 
+    # ---- configs[4]: 448 px prefill (1024 image tokens, L = 1056) on a second context
+    p448 = None
+    if world == 1 and not a.no_448 and a.image_size == 224:
+        del eng
+        torch.cuda.empty_cache()
+        cfg4 = paligemma_3b_config(448)
+        n4 = (448 // 14) ** 2
+        L4 = n4 + 32
+        e4 = Engine(cfg4, device=dev, max_batch=1, max_seq=L4, max_kv=L4 + 8)
+        e4.fill_synthetic(a.seed, init_policy)
+        e4.prepare()
+        px4 = (torch.rand((1, 3, 448, 448), generator=g, device=dev) * 2 - 1).contiguous()
+        ids4 = torch.from_numpy(prompt_ids(cfg4["image_token_index"], n4, cfg4["text_config"]["vocab_size"])).to(dev)
+        kv4 = e4.new_kv(1, L4 + 8)
+        pm, vm, lmm, _ = time_prefill(e4, px4, ids4, torch.arange(L4)[None], kv4, max(5, a.prefill_iters // 4))
+        p448 = {"prefill_ms": round(pm, 3), "prefill_vision_ms": round(vm, 3), "prefill_lm_ms": round(lmm, 3),
+                "prompt_len": L4, "gemm_roofline": gemm_roofline(e4, L4)}
+        del e4
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import weights as OW
@@ -252,6 +308,8 @@ def main():
                          "bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 3)},
+            "prefill_gemm_roofline": prefill_gemms,
+            "prefill_448": p448,
             "cpu_baseline": cpu,
         }
         if bcast_ms is not None:

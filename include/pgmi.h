@@ -122,6 +122,10 @@ int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch
  * run the phases in dependency order (kernels_step.hip).  Same arithmetic, bit-identical
  * results; the per-phase launches are faster on MI355X today. */
 int pgmi_set_decode_fused(pgmi_ctx* ctx, int on);
+/* Prefill graphs (default on): pgmi_vision and pgmi_lm_forward replay a captured hipGraph when
+ * called again with identical pointer and size arguments (the graph is captured on the second
+ * such call; a replay reads the same addresses as the eager call would).  0 = always eager. */
+int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
 /* Sticky status of the fused step, cleared on read: bit 0 = a phase wait timed out (results of
  * that step are invalid). */
 int pgmi_decode_status(pgmi_ctx* ctx, unsigned* status);
@@ -137,9 +141,14 @@ int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* ou
  * 4 final norm + lm_head (+argmax partials; layer ignored). */
 int pgmi_decode_kernel(pgmi_ctx* ctx, int which, int layer, int B, void* stream);
 
-/* Tuning hook: force the prefill GEMM tile configuration (0: 288x64, 1: 288x32, 2: 256x64,
- * 3: 256x32, 4: 128x128, 5: 128x64) and split-K factor for subsequent calls; cfg < 0 restores
- * the automatic plan. */
+/* Launch one prefill GEMM of `layer` over `rows` rows of the context's prefill workspace
+ * (benchmarking the MFMA path in isolation): 0 = gate|up GEMM + GeGLU epilogue
+ * (modeling_gemma.py:134), 1 = down projection (split-K partials, as the prefill runs it). */
+int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* stream);
+
+/* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent
+ * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-19 LDS-DMA panel tiles);
+ * cfg < 0 restores the automatic (measured) plan. */
 int pgmi_tune_gemm(int cfg, int split);
 
 /* ---- single-op entry points (kernel-level parity tests) ---------------------------------- */

@@ -106,9 +106,20 @@ struct pgmi_ctx {
     long step_trace_blocks = 0;
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
+    // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
+    // identical pointer/shape arguments (a replay is the eager call: kernels read the same
+    // addresses at run time), captured on the second such call
+    bool prefill_graph = true;
+    std::map<std::vector<intptr_t>, GraphEntry> pgraphs;
 };
 
 namespace {
+
+void clear_pgraphs(pgmi_ctx* x) {
+    for (auto& kv : x->pgraphs)
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    x->pgraphs.clear();
+}
 
 int n_img(const pgmi_config& c) { return (c.v_image / c.v_patch) * (c.v_image / c.v_patch); }
 
@@ -291,6 +302,7 @@ int pgmi_destroy(pgmi_ctx* x) {
     if (!x) return 0;
     for (auto& kv : x->graphs)
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    clear_pgraphs(x);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->cap_stream) (void)hipStreamDestroy(x->cap_stream);
     delete x;
@@ -314,7 +326,10 @@ int pgmi_bind_weights(pgmi_ctx* x, void* slab) {
     if (!x || !slab) return fail(PGMI_E_ARG, "null argument");
     if (reinterpret_cast<uintptr_t>(slab) % 256 != 0) return fail(PGMI_E_ARG, "weight slab must be 256-byte aligned");
     x->slab = reinterpret_cast<uint8_t*>(slab);
+    for (auto& kv : x->graphs)
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
     x->graphs.clear();
+    clear_pgraphs(x);
     return 0;
 }
 
@@ -451,6 +466,7 @@ int pgmi_prepare(pgmi_ctx* x) {
     for (auto& kv : x->graphs)
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
     x->graphs.clear();
+    clear_pgraphs(x);
     x->prepared = true;
     return 0;
 }
@@ -460,13 +476,57 @@ int64_t pgmi_kv_bytes(const pgmi_ctx* x, int batch, int max_tokens) {
     return (int64_t)x->c.t_layers * 2 * batch * max_tokens * x->c.t_kv_heads * x->c.t_head_dim * 2;
 }
 
+// Run body(stream) eagerly, or replay its captured hipGraph: the first call with a given key
+// runs eagerly (kernel attributes are set on first launch), the second captures, later ones
+// replay.  The key holds every pointer and size the body reads, so a replay is that call.
+extern "C++" {
+template <class F>
+static int run_graphed(pgmi_ctx* x, hipStream_t s, const std::vector<intptr_t>& key, F body) {
+    if (!x->prefill_graph) return body(s);
+    GraphEntry& ge = x->pgraphs[key];
+    if (!ge.exec) {
+        if (ge.seen++ == 0) return body(s);
+        if (x->pgraphs.size() > 64) {  // bound the cache (e.g. fresh buffers every call)
+            clear_pgraphs(x);
+            return body(s);
+        }
+        hipGraph_t g;
+        HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
+        const int rc = body(x->cap_stream);
+        HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
+        if (rc) {
+            (void)hipGraphDestroy(g);
+            return rc;
+        }
+        GraphEntry& ge2 = x->pgraphs[key];
+        HIPCHK(hipGraphInstantiate(&ge2.exec, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        HIPCHK(hipGraphLaunch(ge2.exec, s));
+        return 0;
+    }
+    HIPCHK(hipGraphLaunch(ge.exec, s));
+    return 0;
+}
+}  // extern "C++"
+
+static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats);
+
 int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, void* stream) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;
     const pgmi_config& c = x->c;
     if (B < 1 || B > c.max_batch) return fail(PGMI_E_ARG, "batch exceeds max_batch");
     if (!pixels || !feats) return fail(PGMI_E_ARG, "null argument");
-    hipStream_t s = (hipStream_t)stream;
+    const std::vector<intptr_t> key{1, (intptr_t)pixels, dtype, B, (intptr_t)feats};
+    rc = run_graphed(x, (hipStream_t)stream, key,
+                     [&](hipStream_t st) { return vision_body(x, st, pixels, dtype, B, feats); });
+    if (rc) return rc;
+    LAUNCHCHK();
+    return 0;
+}
+
+static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats) {
+    const pgmi_config& c = x->c;
     const int N = n_img(c), D = c.v_hidden, Iv = c.v_intermediate, rows = B * N;
     const float eps = c.v_ln_eps;
     patchify(s, pixels, dtype == PGMI_DTYPE_F32, B, c.v_channels, c.v_image, c.v_image, c.v_patch, x->kpad, x->vP);
@@ -549,6 +609,10 @@ int pgmi_embed(pgmi_ctx* x, const int64_t* ids, int rows, void* out, void* strea
     return 0;
 }
 
+static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* image_feats, int n_img_rows,
+                   const void* embeds, int B, int L, void* kv, int kv_batch, int kv_max, int kv_start, float* logits,
+                   int logits_rows);
+
 int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, int n_img_rows, const void* embeds,
                     int B, int L, const int64_t* positions, void* kv, int kv_batch, int kv_max, int kv_start,
                     float* logits, int logits_rows, void* stream) {
@@ -560,13 +624,29 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
     if (kv_start < 0 || kv_start + L > kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
     if (kv_start + L > attention_prefill_max_keys(256)) return fail(PGMI_E_ARG, "prefill attention span too long");
     if (!positions || !kv || !logits || (!embeds && !ids)) return fail(PGMI_E_ARG, "null argument");
-    hipStream_t s = (hipStream_t)stream;
+    // host positions -> device (outside any graph: a pageable host copy is not captured)
+    HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)B * L * sizeof(int64_t), hipMemcpyHostToDevice,
+                          (hipStream_t)stream));
+    const std::vector<intptr_t> key{2, (intptr_t)ids, (intptr_t)image_feats, n_img_rows, (intptr_t)embeds, B, L,
+                                    (intptr_t)kv, kv_batch, kv_max, kv_start, (intptr_t)logits, logits_rows};
+    rc = run_graphed(x, (hipStream_t)stream, key, [&](hipStream_t st) {
+        return lm_body(x, st, ids, image_feats, n_img_rows, embeds, B, L, kv, kv_batch, kv_max, kv_start, logits,
+                       logits_rows);
+    });
+    if (rc) return rc;
+    LAUNCHCHK();
+    return 0;
+}
+
+static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* image_feats, int n_img_rows,
+                   const void* embeds, int B, int L, void* kv, int kv_batch, int kv_max, int kv_start, float* logits,
+                   int logits_rows) {
+    const pgmi_config& c = x->c;
     const int H = c.t_hidden, R = B * L, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const int QKVN = (NH + 2 * NKV) * HD;
     const float eps = c.t_rms_eps;
     const float normalizer = bf16_round_host(std::sqrt((float)H));  // torch.tensor(H**0.5, dtype=bf16) (:367)
     const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
-    HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)R * sizeof(int64_t), hipMemcpyHostToDevice, s));
     if (embeds) {
         scale_rows(s, reinterpret_cast<const uint16_t*>(embeds), (long)R * H, normalizer, x->Hs);
     } else {
@@ -720,6 +800,13 @@ static int decode_any(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, voi
     return decode_body(x, s, ids, B, kv, kv_batch, kv_max, launch_keys, logits, next_ids);
 }
 
+int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    x->prefill_graph = on != 0;
+    clear_pgraphs(x);
+    return 0;
+}
+
 int pgmi_set_decode_fused(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
     x->fused = on != 0;
@@ -811,6 +898,35 @@ int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
             int nparts = 0;
             gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps,
                         W(x, "language_model.model.embed_tokens.weight"), c.t_vocab, x->dlogits, x->pmax, x->pidx, &nparts);
+            break;
+        }
+        default: return fail(PGMI_E_ARG, "unknown kernel id");
+    }
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    const pgmi_config& c = x->c;
+    if (rows < 1 || rows > c.max_batch * c.max_seq) return fail(PGMI_E_ARG, "rows exceed the prefill workspace");
+    if (layer < 0 || layer >= c.t_layers) return fail(PGMI_E_ARG, "layer out of range");
+    hipStream_t s = (hipStream_t)stream;
+    const int H = c.t_hidden;
+    switch (which) {
+        case 0: {  // gate|up GEMM + GeGLU epilogue (modeling_gemma.py:134): Tn -> ACT
+            EpiArgs g{};
+            g.out = x->ACT; g.ldo = c.t_intermediate;
+            gemm(s, x->Tn, H, TL(x, layer, "mlp.gate_proj.weight"), H, rows, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
+                 x->ws_bytes, c.t_intermediate);
+            break;
+        }
+        case 1: {  // down GEMM as the prefill runs it: split-K partials (reduced by the next norm)
+            EpiArgs d{};
+            d.res = x->Hs; d.ldr = H; d.out = x->Hs; d.ldo = H;
+            gemm(s, x->ACT, c.t_intermediate, TL(x, layer, "mlp.down_proj.weight"), c.t_intermediate, rows, H,
+                 c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes, 0, true);
             break;
         }
         default: return fail(PGMI_E_ARG, "unknown kernel id");

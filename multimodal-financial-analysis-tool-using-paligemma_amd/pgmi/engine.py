@@ -236,6 +236,10 @@ class Engine:
         """Batch-1 decode as one dataflow launch per token (opt-in) or one launch per phase (default)."""
         N.check(self.lib.pgmi_set_decode_fused(self.ctx, int(bool(on))), "pgmi_set_decode_fused")
 
+    def set_prefill_graph(self, on: bool) -> None:
+        """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
+        N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
+
     def decode_status(self) -> int:
         """Sticky status of the fused decode step (bit 0: a phase wait timed out); cleared on read."""
         st = ctypes.c_uint(0)

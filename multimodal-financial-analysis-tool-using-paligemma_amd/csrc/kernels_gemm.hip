@@ -216,23 +216,25 @@ __device__ __forceinline__ void vm_wait_tiles(int n) {
     }
 }
 
-template <int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
-__global__ void __launch_bounds__(256, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
+template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                    int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
                                                    int n_mt, int n_nt, int krot) {
-    constexpr int WN = 4 / WM;
+    constexpr int WN = NW / WM;
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
     constexpr int PCS = APC + BPC;
-    static_assert(PCS % 4 == 0, "pieces must split evenly over 4 waves");
-    constexpr int GPW = PCS / 4;                    // LDS-DMA instructions per wave per k-tile
+    // LDS-DMA instructions per wave per k-tile; with 8 waves the last few waves re-load a piece
+    // (same bytes to the same LDS address) so every wave issues GPW and one vmcnt count fits all
+    constexpr int GPW = (PCS + NW - 1) / NW;
     constexpr int ABYTES = BM * 128;
     constexpr int SBYTES = (BM + NB * BN) * 128;    // one ring slot
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_p[];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     const int wm = wave / WN, wn = wave % WN;
     // tile coordinates: the M tiles of one N tile share an XCD (blocks b, b+8, ... do), so a
     // weight tile is fetched from HBM once per XCD rather than once per M tile
@@ -256,14 +258,17 @@ __global__ void __launch_bounds__(256, 1) k_gemm_p(const uint16_t* __restrict__ 
     // they do not all hit the same L2 lines (channels) at once
     const int rot = nkt > 0 ? (nt * krot) % nkt : 0;
 
-    // per-lane source rows of this wave's pieces (piece p = wave + 4 i)
+    // per-lane source rows of this wave's pieces (piece p = wave + NW i)
     const uint16_t* src[GPW];
-    int gk[GPW];  // element offset of the lane's chunk inside a 64-wide k-tile
+    int gk[GPW];    // element offset of the lane's chunk inside a 64-wide k-tile
+    int loff[GPW];  // piece offset in a ring slot (wave-uniform)
     const int prow = lane >> 3;
     const int pchunk = lane & 7;
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
-        const int p = wave + 4 * i;
+        int p = wave + NW * i;
+        if (p >= PCS) p -= PCS;  // padding: repeat a piece
+        loff[i] = p * 1024;
         int row;
         const uint16_t* base;
         long ld;
@@ -285,7 +290,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_p(const uint16_t* __restrict__ 
         src[i] = base + (long)row * ld + gk[i];
     }
     // slot image is piece-linear: A pieces first, then B pieces (piece p at p KiB)
-#define PGMI_LDS_AT(slot, i) ((__attribute__((address_space(3))) void*)(smem_p + (slot) * SBYTES + (wave + 4 * (i)) * 1024))
+#define PGMI_LDS_AT(slot, i) ((__attribute__((address_space(3))) void*)(smem_p + (slot) * SBYTES + loff[i]))
     const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
     auto issue = [&](int kt, int slot) {
         kt += rot;
@@ -420,7 +425,12 @@ enum Cfg : int {
     P128x128 = 17, // TM 4, BN 128, 5 slots
     P64x64d = 18,  // TM 2, BN 64,  10 slots
     P128x64d = 19, // 4x1 waves, TM 2, BN 64, 6 slots
-    kNumCfg = 20,
+    // 8 waves (2 per SIMD: one wave's LDS-DMA issue stalls overlap its partner's MFMAs)
+    Q288w = 20,    // 2x4 waves, TM 9,  BN 128, 3 slots
+    Q352w = 21,    // 2x4 waves, TM 11, BN 128, 2 slots
+    Q256w = 22,    // 2x4 waves, TM 8,  BN 128, 3 slots
+    Q288x256 = 23, // 2x4 waves, TM 9,  BN 256, 2 slots
+    kNumCfg = 24,
 };
 
 struct Plan {
@@ -441,8 +451,8 @@ void gemm_force_plan(int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -456,7 +466,7 @@ static Plan choose(int M, int N, int K, bool dual) {
     static const Entry table[] = {
         {288, 2560, 2048, false, P64x64, 1},    // text q|k|v            11.5 us
         {288, 2048, 2048, false, P64x64, 1},    // text o_proj           13.0 us
-        {288, 16384, 2048, true, P288w, 1},     // text gate|up (GeGLU)  50 us
+        {288, 16384, 2048, true, Q288w, 1},     // text gate|up (GeGLU)  44 us
         {288, 2048, 16384, false, P288n, 8},    // text down             38 us
         {256, 3456, 1152, false, P64x64, 1},    // vision q|k|v          10.1 us
         {256, 1152, 1152, false, P64x64, 1},    // vision out_proj        9.9 us
@@ -466,18 +476,18 @@ static Plan choose(int M, int N, int K, bool dual) {
         {256, 2048, 1152, false, P64x64, 1},    // multimodal projector   9.5 us
         {1056, 2560, 2048, false, P128w, 1},    // 448 px text q|k|v     23.7 us
         {1056, 2048, 2048, false, P288n, 2},    // 448 px text o_proj    28.2 us
-        {1056, 16384, 2048, true, P352w, 1},    // 448 px gate|up       165 us
-        {1056, 2048, 16384, false, P288w, 4},   // 448 px down           93 us
-        {1024, 4304, 1152, false, P352w, 2},    // 448 px vision fc1     37.6 us
+        {1056, 16384, 2048, true, Q352w, 1},    // 448 px gate|up       147 us
+        {1056, 2048, 16384, false, Q352w, 4},   // 448 px down           92 us
+        {1024, 4304, 1152, false, Q352w, 2},    // 448 px vision fc1     34 us
         {1024, 3456, 1152, false, P128w, 1},    // 448 px vision q|k|v   23.3 us
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
     // other shapes (batched prefill: M = B x 256 / 288 rows; other image sizes)
-    if (dual) return mk(M <= 256 ? P256w : M <= 288 ? P288w : P352w, 1);
+    if (dual) return mk(M <= 256 ? Q256w : M <= 288 ? Q288w : Q352w, 1);
     if (K >= 8192) return mk(M <= 288 ? P288n : P288w, M <= 288 ? 8 : 4);
     const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (t64 <= 256) return mk(P64x64, 1);
@@ -532,13 +542,13 @@ static void launch_t(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
 
 // panel GEMM launcher: WM x (4/WM) waves, TNW = 16-column fragments per wave (per B operand
 // for plain GEMMs; the dual GEMM splits them over gate and up); EPI < 0: partials only
-template <int WM, int TM, int TNW, int ST, int EPI>
+template <int NW, int WM, int TM, int TNW, int ST, int EPI>
 static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                      const EpiArgs& ea, float* ws, int split, long up_off) {
     constexpr bool DUAL = (EPI == EPI_GEGLU);
     constexpr int NB = DUAL ? 2 : 1;
     constexpr int TN = DUAL ? (TNW >= 2 ? TNW / 2 : 1) : TNW;  // the dual GEMM keeps the B rows per slot
-    constexpr int BM = WM * TM * 16, BN = (4 / WM) * TN * 16;
+    constexpr int BM = WM * TM * 16, BN = (NW / WM) * TN * 16;
     constexpr int STQ = (size_t)ST * (BM + NB * BN) * 128 <= 163840 ? ST : ST - 1;  // fit 160 KiB
     constexpr size_t lds = (size_t)STQ * (BM + NB * BN) * 128;
     static_assert(lds <= 163840, "LDS ring exceeds 160 KiB");
@@ -549,14 +559,14 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     dim3 grid(n_mt * n_nt, split);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<WM, TM, TN, NB, STQ, EK, false>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<WM, TM, TN, NB, STQ, EK, true>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
     if (EPI < 0 || split > 1) {
-        hipLaunchKernelGGL((k_gemm_p<WM, TM, TN, NB, STQ, EK, true>), grid, dim3(256), lds, s, A, lda, W, ldw, M, N, K, per,
+        hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
                            ea, ws, up_off, n_mt, n_nt, g_krot);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
@@ -565,7 +575,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
             hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
         }
     } else {
-        hipLaunchKernelGGL((k_gemm_p<WM, TM, TN, NB, STQ, EK, false>), grid, dim3(256), lds, s, A, lda, W, ldw, M, N, K,
+        hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, n_mt, n_nt, g_krot);
     }
 }
@@ -573,7 +583,8 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
 template <int EPI>
 static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                         const EpiArgs& ea, float* ws, const Plan& p, long up_off) {
-#define P_(wm, tm, tn, st) launch_p<wm, tm, tn, st, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off)
+#define P_(wm, tm, tn, st) launch_p<4, wm, tm, tn, st, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off)
+#define P8_(wm, tm, tn, st) launch_p<8, wm, tm, tn, st, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off)
     switch (p.cfg) {
         case P288w: P_(2, 9, 4, 3); break;
         case P256w: P_(2, 8, 4, 3); break;
@@ -589,9 +600,14 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case P128x128: P_(2, 4, 4, 5); break;
         case P64x64d: P_(2, 2, 2, 10); break;
         case P128x64d: P_(4, 2, 4, 6); break;
+        case Q288w: P8_(2, 9, 2, 3); break;
+        case Q352w: P8_(2, 11, 2, 2); break;
+        case Q256w: P8_(2, 8, 2, 3); break;
+        case Q288x256: P8_(2, 9, 4, 2); break;
         default: break;
     }
 #undef P_
+#undef P8_
 }
 
 template <int EPI>

@@ -120,6 +120,29 @@ def time_prefill(eng, px, ids, pos, kv, iters):
     return statistics.median(pre), e0.elapsed_time(e1), e1.elapsed_time(e2), lg
 
 
+def time_preprocess(eng, dev, size, iters=20):
+    """GPU process_images (pgmi_preprocess: PIL-exact BICUBIC resize + normalize) of one decoded
+    480x640 RGB image already on the device -> float32 pixel_values, HIP events."""
+    import torch
+    from pgmi import _native as N
+    src = torch.randint(0, 256, (480, 640, 3), dtype=torch.uint8, device=dev)
+    out = torch.empty((3, size, size), dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream()
+
+    def run():
+        N.check(eng.lib.pgmi_preprocess(eng.ctx, src.data_ptr(), 480, 640, size, size, out.data_ptr(), s.cuda_stream))
+
+    for _ in range(3):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        run()
+    e1.record(s)
+    e1.synchronize()
+    return round(e0.elapsed_time(e1) / iters, 4)
+
+
 def gemm_roofline(eng, rows, iters=36):
     """The prefill's dominant MFMA GEMMs (gate|up + GeGLU, down) of all 18 layers over `rows`
     token rows, timed with HIP events on the stream they are launched on."""
@@ -193,6 +216,7 @@ def main():
 
     prefill_ms, vision_ms, lm_ms, lg = time_prefill(eng, px, ids, pos, kv, a.prefill_iters)
     prefill_gemms = gemm_roofline(eng, B * L)
+    pre_ms = time_preprocess(eng, dev, a.image_size)
 
     # ---- decode: warmup, then exactly K timed steps (graph replay, device-side argmax)
     first = eng.argmax(lg[:, 0])
@@ -308,6 +332,8 @@ def main():
                          "bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 3)},
+            "preprocess_ms": pre_ms,
+            "preprocess_workload": f"one decoded 480x640 RGB image -> {a.image_size}x{a.image_size} pixel_values (GPU)",
             "prefill_gemm_roofline": prefill_gemms,
             "prefill_448": p448,
             "cpu_baseline": cpu,

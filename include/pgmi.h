@@ -141,6 +141,15 @@ int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* ou
  * 4 final norm + lm_head (+argmax partials; layer ignored). */
 int pgmi_decode_kernel(pgmi_ctx* ctx, int which, int layer, int B, void* stream);
 
+/* Image preprocessing on the GPU (processing_paligemma.py:13-49, process_images): PIL-exact
+ * BICUBIC resize of one decoded RGB image (uint8 HWC, device memory, H x W) to out_h x out_w,
+ * then x/255 (float64 product cast to float32), (x - 0.5)/0.5 and HWC -> CHW, written to
+ * `out_chw` (float32 [3][out_h][out_w], device) -- the reference's pixel_values for one image.
+ * Uses the context's split-K scratch (stream-ordered with the prefill).  JPEG decode stays on
+ * the host. */
+int pgmi_preprocess(pgmi_ctx* ctx, const void* src_hwc, int H, int W, int out_h, int out_w, float* out_chw,
+                    void* stream);
+
 /* Launch one prefill GEMM of `layer` over `rows` rows of the context's prefill workspace
  * (benchmarking the MFMA path in isolation): 0 = gate|up GEMM + GeGLU epilogue
  * (modeling_gemma.py:134), 1 = down projection (split-K partials, as the prefill runs it). */

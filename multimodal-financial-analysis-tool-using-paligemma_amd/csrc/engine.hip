@@ -906,6 +906,18 @@ int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
     return 0;
 }
 
+int pgmi_preprocess(pgmi_ctx* x, const void* src_hwc, int H, int W, int out_h, int out_w, float* out_chw,
+                    void* stream) {
+    if (!x || !src_hwc || !out_chw) return fail(PGMI_E_ARG, "null argument");
+    if (H < 1 || W < 1 || out_h < 1 || out_w < 1) return fail(PGMI_E_ARG, "empty image");
+    if (!x->ws) return fail(PGMI_E_STATE, "workspace not allocated (pgmi_prepare)");
+    if (preprocess_scratch_bytes(H, W, out_h, out_w) > x->ws_bytes)
+        return fail(PGMI_E_ARG, "image too large for the preprocessing scratch");
+    preprocess((hipStream_t)stream, reinterpret_cast<const uint8_t*>(src_hwc), H, W, out_h, out_w, out_chw, x->ws);
+    LAUNCHCHK();
+    return 0;
+}
+
 int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* stream) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;

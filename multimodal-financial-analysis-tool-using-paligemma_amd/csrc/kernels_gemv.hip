@@ -38,7 +38,13 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
     if (B <= 1) {
         const int cap = tune_variant("PGMI_QKV_CAP", 0);
-        if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
+        const int upb = tune_variant("PGMI_QKV_UPB", 0);  // > 0: contiguous slices of upb units
+        if (upb > 0) {
+            a.upb = upb;
+            const int blocks = (a.n_units + upb - 1) / upb;
+            if (tune_variant("PGMI_QKV_DEPTH", 2) == 2) launch_gemv<1, 4, 1, GV_QKV, 1, 2>(s, a, blocks);
+            else launch_gemv<1, 4, 1, GV_QKV>(s, a, blocks);
+        } else if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
         else launch_gemv<1, 4, 1, GV_QKV>(s, a, cap);
     }
     else if (B <= 2) L_(2, 4, 1, GV_QKV);

@@ -110,6 +110,10 @@ void patchify(hipStream_t s, const void* px, int px_is_f32, int B, int C, int H,
               uint16_t* out);
 void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float scale, float offset);
 void set_step(hipStream_t s, StepState* st, int kv_len, int position);
+// PIL-exact BICUBIC resize of a uint8 HWC RGB image + rescale/normalize -> float32 CHW
+// (processing_paligemma.py:13-49); scratch of preprocess_scratch_bytes() on the device
+size_t preprocess_scratch_bytes(int H, int W, int out_h, int out_w);
+void preprocess(hipStream_t s, const uint8_t* src, int H, int W, int out_h, int out_w, float* out, void* scratch);
 void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uint16_t* dst);
 
 

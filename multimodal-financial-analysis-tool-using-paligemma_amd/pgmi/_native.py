@@ -62,6 +62,7 @@ SIGNATURES = {
     "pgmi_set_decode_fused": (i32, [vp, i32]),
     "pgmi_set_prefill_graph": (i32, [vp, i32]),
     "pgmi_prefill_kernel": (i32, [vp, i32, i32, i32, vp]),
+    "pgmi_preprocess": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
     "pgmi_decode_status": (i32, [vp, vp]),
     "pgmi_decode_trace": (i32, [vp, vp, ctypes.c_long]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),

@@ -176,6 +176,22 @@ class Engine:
         N.check(self.lib.pgmi_vision(self.ctx, px.data_ptr(), dt, B, out.data_ptr(), self._s()), "pgmi_vision")
         return out
 
+    def preprocess(self, images, size: Optional[int] = None) -> torch.Tensor:
+        """process_images (processing_paligemma.py:31-50) on the GPU: PIL-exact BICUBIC resize
+        of each decoded RGB image (PIL image or uint8 HWC array), x/255, (x-0.5)/0.5, CHW.
+        Returns pixel_values (B, 3, size, size) float32 on the device."""
+        import numpy as np
+        S = int(size or self.cfgd["v_image"])
+        out = torch.empty((len(images), 3, S, S), dtype=torch.float32, device=self.device)
+        for i, im in enumerate(images):
+            arr = np.asarray(im.convert("RGB") if hasattr(im, "convert") else im, dtype=np.uint8)
+            if arr.ndim != 3 or arr.shape[2] != 3:
+                raise ValueError(f"expected an RGB image (H, W, 3), got {arr.shape}")
+            src = torch.from_numpy(np.array(arr, dtype=np.uint8, order="C")).to(self.device)
+            N.check(self.lib.pgmi_preprocess(self.ctx, src.data_ptr(), arr.shape[0], arr.shape[1], S, S,
+                                             out[i].data_ptr(), self._s()), "pgmi_preprocess")
+        return out
+
     def project(self, feats: torch.Tensor) -> torch.Tensor:
         self._ready()
         f = feats.to(self.device, torch.bfloat16).contiguous()

@@ -2,9 +2,10 @@
 
 Same functions, constants and PaliGemmaProcessor API as /root/reference/processing_paligemma.py
 (:1-117): BICUBIC resize (PIL), x/255, (x - 0.5)/0.5, HWC -> CHW, and the
-"<image>" * N + bos + prompt + "\\n" prompt layout.  Host-side glue, not the GPU hot path
-(SURVEY.md sec.8f ranks GPU preprocessing as "next"); tests/test_cpu_host.py pins it to the
-reference's own outputs on the committed COCO images.
+"<image>" * N + bos + prompt + "\\n" prompt layout; tests/test_cpu_host.py pins it to the
+reference's own outputs on the committed COCO images.  `process_images_gpu` (and
+PaliGemmaProcessor(..., engine=...)) runs the same steps on the MI355X through libpgmi
+(pgmi_preprocess: PIL-exact resample; tests/test_gpu_preprocess.py).
 """
 from __future__ import annotations
 
@@ -53,13 +54,24 @@ def process_images(images: List[Image.Image], size: Dict[str, int] = None, resam
     return out
 
 
+def process_images_gpu(images: List[Image.Image], size: Tuple[int, int], engine) -> torch.Tensor:
+    """process_images with BICUBIC / 1/255 / IMAGENET_STANDARD mean+std on the GPU (the
+    reference's only configuration, processing_paligemma.py:82-89): (B, 3, H, W) float32 on
+    the engine's device, bit-identical to torch.tensor(np.stack(process_images(...)))."""
+    if size[0] != size[1]:
+        raise ValueError("square outputs only (PaliGemma image_size)")
+    return engine.preprocess(images, size=size[0])
+
+
 class PaliGemmaProcessor:
-    """processing_paligemma.py:52-117."""
+    """processing_paligemma.py:52-117.  engine (optional, not in the reference): a pgmi.Engine
+    whose GPU preprocessing produces pixel_values (on the device) instead of PIL + numpy."""
 
     IMAGE_TOKEN = "<image>"
 
-    def __init__(self, tokenizer, num_image_tokens: int, image_size: int):
+    def __init__(self, tokenizer, num_image_tokens: int, image_size: int, engine=None):
         super().__init__()
+        self.engine = engine
         self.image_seq_length = num_image_tokens
         self.image_size = image_size
         tokenizer.add_special_tokens({"additional_special_tokens": [self.IMAGE_TOKEN]})
@@ -73,10 +85,13 @@ class PaliGemmaProcessor:
     def __call__(self, text: List[str], images: List[Image.Image], padding: str = "longest",
                  truncation: bool = True) -> dict:
         assert len(images) == 1 and len(text) == 1, f"Received {len(images)} images for {len(text)} prompts."
-        pixel_values = process_images(images, size=(self.image_size, self.image_size),
-                                      resample=Image.Resampling.BICUBIC, rescale_factor=1 / 255.0,
-                                      image_mean=IMAGENET_STANDARD_MEAN, image_std=IMAGENET_STANDARD_STD)
-        pixel_values = torch.tensor(np.stack(pixel_values, axis=0))
+        if self.engine is not None:
+            pixel_values = process_images_gpu(images, (self.image_size, self.image_size), self.engine)
+        else:
+            pixel_values = process_images(images, size=(self.image_size, self.image_size),
+                                          resample=Image.Resampling.BICUBIC, rescale_factor=1 / 255.0,
+                                          image_mean=IMAGENET_STANDARD_MEAN, image_std=IMAGENET_STANDARD_STD)
+            pixel_values = torch.tensor(np.stack(pixel_values, axis=0))
         input_strings = [add_image_tokens_to_prompt(prefix_prompt=p, bos_token=self.tokenizer.bos_token,
                                                     image_seq_len=self.image_seq_length, image_token=self.IMAGE_TOKEN)
                          for p in text]

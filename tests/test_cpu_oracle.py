@@ -149,3 +149,19 @@ def test_full_size_fixture_consistency(golden_dir):
     assert b["tokens"].shape[-1] == 64
     assert np.array_equal(b["topk_idx"][:, 0], b["tokens"].reshape(-1))
     assert float(f["ref_bf16_rel_l2"].max()) < 0.05
+
+
+def test_resize_oracle_bit_exact_vs_pil(golden_dir):
+    """oracle/resize_np.py (PIL Resample.c restated) vs PIL's outputs in preprocess.npz."""
+    import sys
+    sys.path.insert(0, golden_dir)
+    from make_preprocess import SYNTH, synthetic_image
+    from oracle import resize_np as R
+    g = np.load(os.path.join(golden_dir, "preprocess.npz"))
+    for s in (224, 448):
+        assert np.array_equal(R.resize_bicubic_u8(g["coco0_src"], s, s), g[f"coco0_{s}"])
+    for seed, h, w, s in SYNTH[:4]:
+        assert np.array_equal(R.resize_bicubic_u8(synthetic_image(seed, h, w), s, s), g[f"syn{seed}_{h}x{w}_{s}"])
+    # the COCO fixture agrees with the pixels.npz one (the reference's process_images input)
+    px = np.load(os.path.join(golden_dir, "pixels.npz"))
+    assert np.array_equal(g["coco0_224"], px["u8_0_224"]) and np.array_equal(g["coco0_448"], px["u8_0_448"])

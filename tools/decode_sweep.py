@@ -13,7 +13,7 @@ import torch  # noqa: E402
 from oracle import weights as W  # noqa: E402
 from pgmi import Engine  # noqa: E402
 
-KEYS = ["PGMI_QKV_RPW", "PGMI_QKV_CAP", "PGMI_O_RPW", "PGMI_O_CAP", "PGMI_GU_RPW", "PGMI_GU_CAP", "PGMI_DOWN_RPW",
+KEYS = ["PGMI_QKV_RPW", "PGMI_QKV_CAP", "PGMI_QKV_UPB", "PGMI_QKV_DEPTH", "PGMI_O_RPW", "PGMI_O_CAP", "PGMI_GU_RPW", "PGMI_GU_CAP", "PGMI_DOWN_RPW",
         "PGMI_DOWN_CAP", "PGMI_LM_RPW", "PGMI_LM_CAP"]
 
 

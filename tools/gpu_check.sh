@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 if [ -n "$2" ]; then K="-k $2"; else K=""; fi
-timeout -k 10 600 python -m pytest $R/tests -m gpu -x -q $K > $OUT/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread $K > $OUT/tests.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 $R/bench.py --steps 64 --warmup 8 --no-cpu-baseline --prefill-iters 5 > $OUT/bench.log 2>&1

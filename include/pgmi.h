@@ -160,6 +160,21 @@ int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* str
  * cfg < 0 restores the automatic (measured) plan. */
 int pgmi_tune_gemm(int cfg, int split);
 
+/* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
+ * LDS-resident scores, RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
+ * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); -1 restores the measured choice. */
+int pgmi_tune_attention(int variant);
+
+/* Nucleus sampling, inference.py:15-24 (_sample_top_p) with inference.py:65's
+ * softmax(logits / temperature) fused when temperature > 0 (temperature <= 0: x already holds
+ * the probabilities, _sample_top_p's own input).  x: device fp32 [rows][V]; u: device fp32
+ * [rows] uniforms in [0, 1) that replace torch.multinomial's internal draw (the token is the
+ * first position of the descending order whose cumulative kept mass exceeds u * Z; equal
+ * probabilities in index order); out: device int64 [rows]; kept_mass (device fp32 [rows], may
+ * be NULL): Z, the renormalisation mass of :21.  Scratch: the context's split-K workspace. */
+int pgmi_sample_top_p(pgmi_ctx* ctx, const float* x, int rows, int V, float temperature, float top_p,
+                      const float* u, int64_t* out, float* kept_mass, void* stream);
+
 /* ---- single-op entry points (kernel-level parity tests) ---------------------------------- */
 /* out = epilogue(A[M,K] . W[N,K]^T): epi 0 store, 1 +bias, 2 +bias,gelu, 3 +bias,+res, 4 +res,
  * 6 fp32 out (out is float*), 7 GeGLU with up rows at W + N*K */

@@ -622,7 +622,6 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
     if (B < 1 || B > c.max_batch || B > kv_batch) return fail(PGMI_E_ARG, "batch exceeds capacity");
     if (L < 1 || L > c.max_seq) return fail(PGMI_E_ARG, "sequence length exceeds max_seq");
     if (kv_start < 0 || kv_start + L > kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
-    if (kv_start + L > attention_prefill_max_keys(256)) return fail(PGMI_E_ARG, "prefill attention span too long");
     if (!positions || !kv || !logits || (!embeds && !ids)) return fail(PGMI_E_ARG, "null argument");
     // host positions -> device (outside any graph: a pageable host copy is not captured)
     HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)B * L * sizeof(int64_t), hipMemcpyHostToDevice,
@@ -953,6 +952,28 @@ int pgmi_tune_gemm(int cfg, int split) {
     return 0;
 }
 
+int pgmi_tune_attention(int variant) {
+    static const int ok[] = {-1, 0, 41, 42, 21, 22, 44, 24};
+    for (int v : ok)
+        if (v == variant) {
+            attention_force_variant(variant);
+            return 0;
+        }
+    return fail(PGMI_E_ARG, "unknown attention variant");
+}
+
+int pgmi_sample_top_p(pgmi_ctx* x, const float* logits, int rows, int V, float temperature, float top_p,
+                      const float* u, int64_t* out, float* kept_mass, void* stream) {
+    if (!x || !logits || !u || !out) return fail(PGMI_E_ARG, "null argument");
+    if (rows <= 0 || V <= 0) return fail(PGMI_E_ARG, "sample_top_p: empty probabilities");
+    if (!(top_p >= 0.f)) return fail(PGMI_E_ARG, "sample_top_p: top_p must be >= 0");
+    if (!x->ws) return fail(PGMI_E_STATE, "workspace not allocated (pgmi_prepare)");
+    if ((size_t)rows * V * sizeof(float) > x->ws_bytes) return fail(PGMI_E_ARG, "sample_top_p: rows x vocab exceed the scratch");
+    sample_top_p((hipStream_t)stream, logits, rows, V, temperature, top_p, u, x->ws, out, kept_mass);
+    LAUNCHCHK();
+    return 0;
+}
+
 // ---------------------------------------------------------------- single ops (tests)
 int pgmi_op_gemm(pgmi_ctx* x, const void* A, const void* Wt, int M, int N, int K, int epi, const void* bias,
                  const void* res, void* out, void* stream) {
@@ -994,7 +1015,6 @@ int pgmi_op_attention(pgmi_ctx* x, const void* q, const void* k, const void* v, 
     if (!x) return fail(PGMI_E_ARG, "null ctx");
     if (hd != 256 && hd != 72) return fail(PGMI_E_ARG, "head_dim must be 72 or 256");
     if (H % Hkv != 0 || H / Hkv > 16) return fail(PGMI_E_ARG, "bad head grouping");
-    if (Lk > attention_prefill_max_keys(hd)) return fail(PGMI_E_ARG, "too many keys");
     AttnArgs a{};
     a.q = reinterpret_cast<const uint16_t*>(q); a.q_b_stride = (long)Lq * H * hd; a.q_row_stride = H * hd; a.q_head_stride = hd;
     a.k = reinterpret_cast<const uint16_t*>(k); a.k_b_stride = (long)Lk * Hkv * hd; a.k_row_stride = Hkv * hd; a.k_head_stride = hd;

@@ -18,6 +18,8 @@
 #include "common.h"
 #include "launch.h"
 
+#include <cstdlib>
+
 namespace pgmi {
 
 
@@ -183,6 +185,279 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- prefill, K/V-tiled (two pass)
+// One workgroup = RG x 16 query rows (RG waves, one 16-row group each) x all keys, K/V streamed
+// through LDS in 32-key tiles that every wave of the workgroup shares (the 16-row kernel above
+// re-read the whole K and V from L2 for every 16 rows).  KSPL key-split groups of RG waves
+// take alternate tiles and meet in LDS at the two combine points.  No score matrix is kept,
+// so the key count is unbounded; the reference's rounding points stay exact:
+//   pass 1: s = bf16(bf16(k.q) * scale) per tile, lane-local online (max, sum exp) -> per-row
+//           M, L after a fixed-order combine (lanes, then split groups);
+//   pass 2: s recomputed, p = bf16(exp(s - M) / L) (the reference's bf16(softmax_f32)),
+//           O += p.V on MFMA, O summed over split groups in a fixed order, rounded once.
+// Scores are computed transposed, S^T = K Q^T (A = K rows from LDS, B = Q fragments held in
+// registers): lane (g = lane >> 4) then holds query (lane & 15) x keys {4g..4g+3, 16+4g..16+4g+3}
+// of the tile, which is exactly an A fragment of P for the P.V MFMA under the k-slot order
+// j<4 -> 4g+j, j>=4 -> 16+4g+j-4; the V operand is read in that key order by transposed LDS reads.
+// K rows in LDS: 16-B chunk c of row r at chunk (c ^ (r & 15)) -- conflict-free ds_read_b128 of
+// 16 rows x one 64-B k slice; rows padded with zero chunks to 16 (HD 72) / 32 (HD 256) chunks.
+template <int HD>
+struct FAInfo {
+    static constexpr int KS = (HD + 31) / 32;                  // 32-deep k-steps of K.Q
+    static constexpr int CT = (HD + 15) / 16;                  // 16-wide output tiles of P.V
+    static constexpr int CH = (HD + 7) / 8;                    // 16-B chunks of a head row
+    static constexpr int KRC = KS * 4 <= 16 ? 16 : KS * 4;     // K row chunks in LDS (>= 16 for the swizzle)
+    static constexpr int KRS = KRC * 8;                        // K row stride (elements)
+    static constexpr int VS = (CT * 16 + 127) / 128 * 128 + 16;  // V row stride: 8 mod 64 dwords
+};
+
+__device__ __forceinline__ float fa_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// combine two (max, sum-of-exp) pairs (exact when one side is empty)
+__device__ __forceinline__ void fa_comb(float& m, float& l, float m2, float l2) {
+    const float M = fmaxf(m, m2);
+    if (M == -INFINITY) return;
+    l = (m == -INFINITY ? 0.f : l * fa_exp(m - M)) + (m2 == -INFINITY ? 0.f : l2 * fa_exp(m2 - M));
+    m = M;
+}
+
+template <int HD, int RG, int KSPL>
+__global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
+    using I = FAInfo<HD>;
+    constexpr int KS = I::KS, CT = I::CT, CH = I::CH, KRC = I::KRC, KRS = I::KRS, VS = I::VS;
+    constexpr int TK = 32;                                 // keys per tile
+    constexpr int NTH = 64 * RG;                           // threads of one split group
+    constexpr int LCH = (TK * CH + NTH - 1) / NTH;         // 16-B chunks per thread per tile (K; V alike)
+    constexpr int KBUF = TK * KRS, VBUF = TK * VS;         // elements per buffer
+    constexpr int GRP = 2 * (KBUF + VBUF);                 // elements per split group (2 buffers each)
+    extern __shared__ __attribute__((aligned(16))) uint16_t fsm[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = wave % RG, ks = wave / RG, th = tid % NTH;
+    const int g = lane >> 4, li = lane & 15;
+    uint16_t* Kl = fsm + ks * GRP;
+    uint16_t* Vl = Kl + 2 * KBUF;
+    float* stat = reinterpret_cast<float*>(fsm + KSPL * GRP);  // [KSPL][RG][16][2]
+
+    const int b = blockIdx.z, kvh = blockIdx.y;
+    const int nrows = a.Lq * a.G;
+    const int qi = blockIdx.x * (16 * RG) + rg * 16 + li;
+    const bool qvalid = qi < nrows;
+    const int qpos = qvalid ? qi / a.G : 0, qhead = kvh * a.G + (qvalid ? qi % a.G : 0);
+    const uint16_t* qrow = a.q + b * a.q_b_stride + (long)qpos * a.q_row_stride + qhead * a.q_head_stride;
+    short8 qf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) qf[kk] = load_frag<HD>(qrow, qvalid, kk, lane);
+
+    // zero the K pad chunks once (never written by tile stores; k-steps past HD read them)
+    if constexpr (KRC > CH) {
+        for (int e = th; e < 2 * TK * (KRC - CH); e += NTH) {
+            const int r = e / (KRC - CH), c = CH + e % (KRC - CH);  // r over both buffers' rows
+            *reinterpret_cast<uint4*>(Kl + r * KRS + ((c ^ (r & 15)) << 3)) = make_uint4(0, 0, 0, 0);
+        }
+    }
+
+    const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
+    const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
+    const int nt = (a.Lk + TK - 1) / TK;
+    const int nit = (nt + KSPL - 1) / KSPL;  // tiles per split group (every group runs nit barriers)
+
+    uint4 kr[LCH], vr[LCH];
+    auto gload = [&](int t, bool withv) {
+#pragma unroll
+        for (int i = 0; i < LCH; ++i) {
+            const int e = th + NTH * i;
+            const int key = t * TK + e / CH, ch = e % CH;
+            const bool ok = e < TK * CH && t < nt && key < a.Lk;
+            kr[i] = ok ? ldg16(kbase + (long)key * a.k_row_stride + ch * 8) : make_uint4(0, 0, 0, 0);
+            if (withv) vr[i] = ok ? ldg16(vbase + (long)key * a.v_row_stride + ch * 8) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto lstore = [&](int buf, bool withv) {
+#pragma unroll
+        for (int i = 0; i < LCH; ++i) {
+            const int e = th + NTH * i;
+            if (e < TK * CH) {
+                const int r = e / CH, ch = e % CH;
+                *reinterpret_cast<uint4*>(Kl + buf * KBUF + r * KRS + ((ch ^ (r & 15)) << 3)) = kr[i];
+                if (withv) *reinterpret_cast<uint4*>(Vl + buf * VBUF + r * VS + ch * 8) = vr[i];
+            }
+        }
+    };
+    // S^T for the 32 keys of the tile in buffer buf: s[kt][r] = key t*32 + 16kt + 4g + r, query li
+    auto scores = [&](int buf, int t, float (&s)[2][4]) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+            const int r = kt * 16 + li;
+            const uint16_t* kp = Kl + buf * KBUF + r * KRS;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                const short8 kf = *reinterpret_cast<const short8*>(kp + (((kk * 4 + g) ^ (r & 15)) << 3));
+                acc = mfma16(kf, qf[kk], acc);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = t * TK + kt * 16 + 4 * g + j;
+                s[kt][j] = key < a.Lk ? rbf(rbf(acc[j]) * a.scale) : -INFINITY;
+            }
+        }
+    };
+
+    // ---- pass 1: per-row max and sum of exp
+    float m = -INFINITY, l = 0.f;
+    gload(ks, false);
+    lstore(0, false);
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+        const int t = it * KSPL + ks, buf = it & 1;
+        if (it + 1 < nit) gload(t + KSPL, false);
+        float s[2][4];
+        scores(buf, t, s);
+        float tm = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tm = fmaxf(tm, s[kt][j]);
+        const float mn = fmaxf(m, tm);
+        if (mn != -INFINITY) {
+            float ts = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ts += fa_exp(s[kt][j] - mn);
+            l = (m == -INFINITY ? 0.f : l * fa_exp(m - mn)) + ts;
+            m = mn;
+        }
+        if (it + 1 < nit) lstore(buf ^ 1, false);
+        __syncthreads();
+    }
+    // lanes g = 0..3 of a query, in a fixed order
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+        const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+        if (lane & o) fa_comb(m, l, m2, l2);  // the higher lane group folds the lower one in ...
+        else {
+            float mm = m2, ll = l2;
+            fa_comb(mm, ll, m, l);            // ... the same way, so both sides agree bitwise
+            m = mm;
+            l = ll;
+        }
+    }
+    if constexpr (KSPL > 1) {
+        if (g == 0) {
+            stat[((ks * RG + rg) * 16 + li) * 2 + 0] = m;
+            stat[((ks * RG + rg) * 16 + li) * 2 + 1] = l;
+        }
+        __syncthreads();
+        m = stat[(rg * 16 + li) * 2 + 0];
+        l = stat[(rg * 16 + li) * 2 + 1];
+#pragma unroll
+        for (int q = 1; q < KSPL; ++q)
+            fa_comb(m, l, stat[((q * RG + rg) * 16 + li) * 2 + 0], stat[((q * RG + rg) * 16 + li) * 2 + 1]);
+    }
+    const float invl = 1.0f / l;
+
+    // ---- pass 2: O = sum over tiles of bf16(p) . V
+    f32x4 oacc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gload(ks, true);
+    lstore(0, true);
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+        const int t = it * KSPL + ks, buf = it & 1;
+        if (it + 1 < nit) gload(t + KSPL, true);
+        float s[2][4];
+        scores(buf, t, s);
+        short8 pa;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pa[kt * 4 + j] = (short)f2bf(fa_exp(s[kt][j] - m) * invl);
+        const uint16_t* vb0 = Vl + buf * VBUF + (4 * g + (li >> 2)) * VS + 4 * (li & 3);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s4v*)(vb0 + c * 16));
+            const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s4v*)(vb0 + 16 * VS + c * 16));
+            const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            oacc[c] = mfma16(pa, vb, oacc[c]);
+        }
+        if (it + 1 < nit) lstore(buf ^ 1, true);
+        __syncthreads();
+    }
+    // split groups 1.. hand their partial O to group 0 through LDS (the tile buffers are free)
+    if constexpr (KSPL > 1) {
+        float* ob = reinterpret_cast<float*>(fsm);
+        static_assert((size_t)(KSPL - 1) * RG * CT * 64 * 16 <= (size_t)KSPL * GRP * 2, "O exchange fits");
+        if (ks > 0) {
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+                *reinterpret_cast<f32x4*>(ob + ((((ks - 1) * RG + rg) * CT + c) * 64 + lane) * 4) = oacc[c];
+        }
+        __syncthreads();
+        if (ks > 0) return;
+#pragma unroll
+        for (int q = 1; q < KSPL; ++q)
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+                oacc[c] += *reinterpret_cast<const f32x4*>(ob + ((((q - 1) * RG + rg) * CT + c) * 64 + lane) * 4);
+    }
+    // C map: d = 16c + li, query row 4g + r of the wave's 16
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int d = c * 16 + li;
+        if (d >= HD) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = blockIdx.x * (16 * RG) + rg * 16 + 4 * g + r;
+            if (i >= nrows) continue;
+            const int pos = i / a.G, head = kvh * a.G + i % a.G;
+            a.o[b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + d] = f2bf(oacc[c][r]);
+        }
+    }
+}
+
+template <int HD, int RG, int KSPL>
+static void launch_fa(hipStream_t s, const AttnArgs& a) {
+    using I = FAInfo<HD>;
+    constexpr size_t lds = (size_t)KSPL * 2 * 32 * (I::KRS + I::VS) * 2 + (size_t)KSPL * RG * 16 * 2 * 4;
+    static_assert(lds <= 160 * 1024, "LDS");
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fa<HD, RG, KSPL>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    dim3 grid((a.Lq * a.G + 16 * RG - 1) / (16 * RG), a.n_kv, a.B);
+    hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL>), grid, dim3(64 * RG * KSPL), lds, s, a);
+}
+
+// attention variant override (tuning hook pgmi_tune_attention / env PGMI_ATTN): 0 = the 16-row
+// kernel, RK = the tiled kernel with RG = R, KSPL = K (41, 42, 21, 22; 44 and 24 for HD 72);
+// -1 = the measured choice in attention_prefill
+static int g_attn_force = [] {
+    const char* e = std::getenv("PGMI_ATTN");
+    return e ? std::atoi(e) : -1;
+}();
+
+void attention_force_variant(int v) { g_attn_force = v; }
+
+template <int HD>
+static void launch_fa_variant(hipStream_t s, const AttnArgs& a, int v) {
+    switch (v) {
+        case 41: launch_fa<HD, 4, 1>(s, a); return;
+        case 21: launch_fa<HD, 2, 1>(s, a); return;
+        case 22: launch_fa<HD, 2, 2>(s, a); return;
+        case 44: if constexpr (HD == 72) { launch_fa<HD, 4, 4>(s, a); return; } break;
+        case 24: if constexpr (HD == 72) { launch_fa<HD, 2, 4>(s, a); return; } break;
+        default: break;
+    }
+    launch_fa<HD, 4, 2>(s, a);
+}
+
 static size_t attn_full_lds(int head_dim, int Lk) {
     const int LkP = (Lk + 31) & ~31;
     const int hdp = (head_dim + 15) / 16 * 16;
@@ -190,6 +465,23 @@ static size_t attn_full_lds(int head_dim, int Lk) {
 }
 
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
+    int v = g_attn_force;
+    if (v < 0) {
+        // measured on MI355X (tools/probes/attn_bench.py, round 1), us per call:
+        //   SigLIP 224 (256 rows x 16 heads):  16-row 16.4 | RG2xKSPL4 10.8 | RG4xKSPL2 13.5
+        //   SigLIP 448 (1024 x 16):            16-row 153.5 | RG4xKSPL4 32.4 | RG4xKSPL2 36.0
+        //   Gemma 224 (288 x 8 heads, MQA):    16-row 21.9 | RG4xKSPL2 26.1 | RG2xKSPL2 26.4
+        //   Gemma 448 (1056 x 8):              16-row 159.5 | RG4xKSPL2 61.3 | RG2xKSPL2 122.7
+        // few rows -> the 16-row kernel (Gemma) or more, smaller workgroups (SigLIP)
+        const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
+        if (head_dim == 256) v = rows <= 4096 ? 0 : 42;
+        else v = rows <= 8192 ? 24 : 44;
+    }
+    if (v != 0 || a.Lk > attention_prefill_max_keys(head_dim)) {
+        if (head_dim == 256) launch_fa_variant<256>(s, a, v);
+        else launch_fa_variant<72>(s, a, v);
+        return;
+    }
     const size_t lds = attn_full_lds(head_dim, a.Lk);
     dim3 grid((a.Lq * a.G + 15) / 16, a.n_kv, a.B);
     if (head_dim == 256) {

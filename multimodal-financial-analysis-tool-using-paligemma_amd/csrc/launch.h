@@ -85,6 +85,7 @@ constexpr int kAttnChunk = 64;
 constexpr int kAttnPartStride = 16 * 256 + 32;  // floats per (b, kv head, chunk) record
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
+void attention_force_variant(int v);  // tuning hook (kernels_attn.hip); -1 = measured choice
 
 // ---------------------------------------------------------------- misc
 // Fused consumer of a projection + residual: if split > 1, h = bf16(bf16(sum_z ws[z] (+bias)) + h)
@@ -115,6 +116,9 @@ void set_step(hipStream_t s, StepState* st, int kv_len, int position);
 size_t preprocess_scratch_bytes(int H, int W, int out_h, int out_w);
 void preprocess(hipStream_t s, const uint8_t* src, int H, int W, int out_h, int out_w, float* out, void* scratch);
 void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uint16_t* dst);
+// nucleus sampling (kernels_sample.hip; inference.py:15-24, :65): scratch = rows x V fp32
+void sample_top_p(hipStream_t s, const float* x, int rows, int V, float temperature, float top_p, const float* u,
+                  float* scratch, int64_t* out, float* kept_mass);
 
 
 // ---- fused decode step (kernels_step.hip): batch 1, one launch per token

@@ -268,13 +268,37 @@ class Engine:
         N.check(self.lib.pgmi_argmax(self.ctx, l2.data_ptr(), l2.shape[0], l2.shape[1], out.data_ptr(), self._s()))
         return out
 
+    def sample_top_p(self, x: torch.Tensor, top_p: float, temperature: Optional[float] = None,
+                     u: Optional[torch.Tensor] = None, generator: Optional[torch.Generator] = None,
+                     return_kept_mass: bool = False):
+        """Nucleus sampling on the device (inference.py:15-24).
+        x (..., V) fp32: logits when `temperature` > 0 (softmax(x / T) of inference.py:65 is
+        fused), else probabilities (the reference _sample_top_p's input).  u: uniforms in [0, 1)
+        per row (default: torch.rand on the device with `generator`).  Returns int64 (rows,)."""
+        x2 = x.reshape(-1, x.shape[-1]).to(self.device, torch.float32).contiguous()
+        rows, V = x2.shape
+        if u is None:
+            u = torch.rand(rows, device=self.device, generator=generator)
+        u = u.to(self.device, torch.float32).reshape(-1).contiguous()
+        if u.numel() != rows:
+            raise ValueError(f"need one uniform per row: {u.numel()} != {rows}")
+        out = torch.empty(rows, dtype=torch.int64, device=self.device)
+        kept = torch.empty(rows, dtype=torch.float32, device=self.device) if return_kept_mass else None
+        T = float(temperature) if temperature is not None and temperature > 0 else 0.0
+        N.check(self.lib.pgmi_sample_top_p(self.ctx, x2.data_ptr(), rows, V, T, float(top_p), u.data_ptr(),
+                                           out.data_ptr(), N.ptr(kept), self._s()), "pgmi_sample_top_p")
+        return (out, kept) if return_kept_mass else out
+
     # ------------------------------------------------------------------ batched greedy driver
     @torch.no_grad()
     def generate(self, input_ids: torch.Tensor, pixel_values: torch.Tensor, n_tokens: int, graph: bool = True,
-                 kv: torch.Tensor = None):
-        """Batched greedy generation: prefill, then n_tokens-1 decode
-        steps with device-side argmax and no host sync per token.  Positions follow
-        inference.py's semantics (first decode position = L + 1, modeling_gemma.py:526)."""
+                 kv: torch.Tensor = None, do_sample: bool = False, temperature: float = 0.8, top_p: float = 0.9,
+                 generator: Optional[torch.Generator] = None):
+        """Batched generation: prefill, then n_tokens-1 decode steps
+        with the next token picked on the device -- greedy argmax, or with do_sample the
+        temperature + top-p draw of inference.py:64-66 -- and no host sync per token.
+        Positions follow inference.py's semantics (first decode position = L + 1,
+        modeling_gemma.py:526)."""
         ids = input_ids.to(self.device, torch.int64)
         B, L = ids.shape
         if kv is None:
@@ -282,12 +306,18 @@ class Engine:
         feats = self.project(self.vision(pixel_values))
         logits = self.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=1)
         toks = torch.empty((B, n_tokens), dtype=torch.int64, device=self.device)
-        toks[:, 0] = self.argmax(logits[:, 0])
+        if do_sample:
+            us = torch.rand((n_tokens, B), device=self.device, generator=generator)
+            toks[:, 0] = self.sample_top_p(logits[:, 0], top_p, temperature, u=us[0])
+        else:
+            toks[:, 0] = self.argmax(logits[:, 0])
         step_logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
         nxt = torch.empty(B, dtype=torch.int64, device=self.device)
         cur = toks[:, 0].clone()
         for t in range(1, n_tokens):
             self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=nxt, graph=graph)
+            if do_sample:
+                nxt = self.sample_top_p(step_logits, top_p, temperature, u=us[t])
             toks[:, t] = nxt
             cur.copy_(nxt)
         return toks

@@ -148,6 +148,10 @@ def _attn_ref(q, k, v, scale):
     (1, 288, 288, 8, 1, 256, 1 / 16),          # Gemma prefill (MQA)
     (2, 33, 70, 8, 1, 256, 1 / 16),            # ragged, keys beyond queries (cache)
     (1, 1, 290, 8, 1, 256, 1 / 16),            # one query position
+    (1, 1024, 1024, 16, 16, 72, 72 ** -0.5),   # SigLIP 448
+    (1, 1056, 1056, 8, 1, 256, 1 / 16),        # Gemma 448 prefill
+    (1, 40, 2100, 8, 1, 256, 1 / 16),          # keys past the old LDS-resident score limit
+    (3, 17, 5, 16, 16, 72, 72 ** -0.5),        # fewer keys than one tile
 ])
 def test_attention_prefill(eng, B, Lq, Lk, H, Hkv, d, scale):
     from pgmi import _native as NN

@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-448", action="store_true", help="skip the 448 px prefill measurement (configs[4])")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the configs[2] (no KV cache) and configs[3] (8 images per GPU) measurements")
+    ap.add_argument("--nokv-tokens", type=int, default=16)
     return ap.parse_args()
 
 
@@ -169,6 +172,89 @@ def gemm_roofline(eng, rows, iters=36):
     return out
 
 
+def time_no_kv(eng, px, ids, tokens):
+    """BASELINE configs[2]: KV cache disabled with ablation semantics
+    (ablation_study_fixed.py:244-251): every token re-runs the vision tower (pixel_values are
+    passed again) and a full non-causal forward over prompt + generated tokens, last-row
+    logits, greedy pick.  Returns ms per token over `tokens` tokens."""
+    import torch
+    L = ids.shape[1]
+    kv = eng.scratch_kv(1, L + tokens)
+
+    def run():
+        cur = ids
+        for _ in range(tokens):
+            feats = eng.project(eng.vision(px))
+            lg = eng.lm_forward(kv, 0, torch.arange(cur.shape[1])[None], ids=cur, image_feats=feats, logits_rows=1)
+            cur = torch.cat([cur, eng.argmax(lg[:, 0])[:, None]], 1)
+        return cur
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / tokens
+
+
+def time_sampling(eng, V, iters=20):
+    """Device top-p draw (inference.py:64-66, T = 0.8, p = 0.9) over one row of V logits."""
+    import torch
+    g = torch.Generator(device=eng.device).manual_seed(0)
+    lg = torch.randn((1, V), device=eng.device, generator=g) * 4
+    u = torch.rand((iters + 3, 1), device=eng.device, generator=g)
+    for i in range(3):
+        eng.sample_top_p(lg, 0.9, 0.8, u=u[i])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(iters):
+        eng.sample_top_p(lg, 0.9, 0.8, u=u[3 + i])
+    e1.record()
+    e1.synchronize()
+    return round(e0.elapsed_time(e1) * 1e3 / iters, 2)
+
+
+def time_batch(cfg, dev, seed, g, B, steps, warmup):
+    """BASELINE configs[3], per GPU: B images (8 of the 64) through a B-row prefill, then
+    lock-step KV-cached greedy decode of B sequences (graph replay, device argmax)."""
+    import torch
+    from pgmi import Engine
+    from pgmi.synthetic import init_policy, prompt_ids
+    n_img = (cfg["vision_config"]["image_size"] // 14) ** 2
+    L = n_img + 32
+    cap = ((L + warmup + steps + 8) + 63) // 64 * 64
+    e = Engine(cfg, device=dev, max_batch=B, max_seq=L, max_kv=cap)
+    e.fill_synthetic(seed, init_policy)
+    e.prepare()
+    px = (torch.rand((B, 3, 224, 224), generator=g, device=dev) * 2 - 1).contiguous()
+    ids = torch.from_numpy(prompt_ids(cfg["image_token_index"], n_img, cfg["text_config"]["vocab_size"])).to(dev)
+    ids = ids.expand(B, -1).contiguous()
+    kv = e.new_kv(B, cap)
+    pm, _, _, lg = time_prefill(e, px, ids, torch.arange(L).expand(B, L), kv, 5)
+    cur = e.argmax(lg[:, 0])
+    nxt = torch.empty_like(cur)
+    logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device=dev)
+    step = 0
+
+    def decode_step():
+        nonlocal step
+        step += 1
+        e.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=nxt, graph=True)
+        cur.copy_(nxt)
+    for _ in range(warmup):
+        decode_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        decode_step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del e
+    torch.cuda.empty_cache()
+    return {"images_per_gpu": B, "prefill_ms": round(pm, 3), "decode_tok_s": round(B * steps / dt, 1),
+            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps}
+
+
 def main():
     a = parse()
     import torch
@@ -191,7 +277,7 @@ def main():
     L = n_img + 32
     B = a.batch
     kv_cap = ((L + a.warmup + a.steps + 8) + 63) // 64 * 64
-    eng = Engine(cfg, device=dev, max_batch=B, max_seq=L, max_kv=kv_cap)
+    eng = Engine(cfg, device=dev, max_batch=B, max_seq=L + a.nokv_tokens, max_kv=kv_cap)
 
     # ---- weights: rank 0 generates, RCCL broadcast of the packed slab over xGMI
     bcast_ms = None
@@ -277,11 +363,25 @@ def main():
         except Exception:
             traffic = None
 
+    # ---- configs[2]: no KV cache (ablation semantics), top-p sampling cost, then configs[3]
+    nokv = None
+    sample_us = time_sampling(eng, cfg["text_config"]["vocab_size"])
+    if world == 1 and not a.no_extra and B == 1:
+        ms_tok = time_no_kv(eng, px[:1], ids[:1], a.nokv_tokens)
+        nokv = {"tokens": a.nokv_tokens, "ms_per_token": round(ms_tok, 3), "tok_s": round(1e3 / ms_tok, 1),
+                "semantics": "vision re-run + full forward over prompt + generated tokens per token"}
+    batch8 = None
+    if world == 1 and not a.no_extra and B == 1:
+        del eng
+        torch.cuda.empty_cache()
+        batch8 = time_batch(cfg, dev, a.seed, g, 8, 64, 8)
+
     # ---- configs[4]: 448 px prefill (1024 image tokens, L = 1056) on a second context
     p448 = None
     if world == 1 and not a.no_448 and a.image_size == 224:
-        del eng
-        torch.cuda.empty_cache()
+        if batch8 is None:
+            del eng
+            torch.cuda.empty_cache()
         cfg4 = paligemma_3b_config(448)
         n4 = (448 // 14) ** 2
         L4 = n4 + 32
@@ -336,6 +436,9 @@ def main():
             "preprocess_workload": f"one decoded 480x640 RGB image -> {a.image_size}x{a.image_size} pixel_values (GPU)",
             "prefill_gemm_roofline": prefill_gemms,
             "prefill_448": p448,
+            "config3_no_kv": nokv,
+            "config4_images_per_gpu": batch8,
+            "sample_top_p_us": sample_us,
             "cpu_baseline": cpu,
         }
         if bcast_ms is not None:

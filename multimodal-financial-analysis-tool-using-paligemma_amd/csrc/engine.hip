@@ -731,10 +731,10 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         a.Lq = 1; a.Lk = 0; a.G = NH / NKV; a.n_kv = NKV; a.B = B; a.scale = 1.0f / std::sqrt((float)HD);
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                    nullptr);
+                    B >= gemv_mf_min_batch() ? x->dAO : nullptr);
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                    c.t_intermediate, x->dACT);
-        gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH);
+        gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
     }
     int nparts = 0;
     gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax, x->pidx,
@@ -887,12 +887,12 @@ int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
     const float eps = c.t_rms_eps;
     const int H = c.t_hidden;
     switch (which) {
-        case 1: gemv_res(s, B, c.t_heads * c.t_head_dim, x->dAO, TL(x, layer, "self_attn.o_proj.weight"), H, x->dH); break;
+        case 1: gemv_res(s, B, c.t_heads * c.t_head_dim, x->dAO, TL(x, layer, "self_attn.o_proj.weight"), H, x->dH, x->ws); break;
         case 2:
             gemv_geglu(s, B, x->dH, TL(x, layer, "post_attention_layernorm.weight"), eps, TL(x, layer, "mlp.gate_proj.weight"),
                        c.t_intermediate, x->dACT);
             break;
-        case 3: gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, layer, "mlp.down_proj.weight"), H, x->dH); break;
+        case 3: gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, layer, "mlp.down_proj.weight"), H, x->dH, x->ws); break;
         case 4: {
             int nparts = 0;
             gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps,
@@ -1030,8 +1030,10 @@ int pgmi_op_gemv_res(pgmi_ctx* x, const void* in, const void* Wt, int B, int N, 
     if (!x) return fail(PGMI_E_ARG, "null ctx");
     if (K != 2048 && K != 16384) return fail(PGMI_E_ARG, "K must be 2048 or 16384");
     if (B < 1 || B > 8) return fail(PGMI_E_ARG, "B must be in [1, 8]");
+    if (!x->ws) return fail(PGMI_E_STATE, "workspace not allocated (pgmi_prepare)");
+    if ((size_t)4 * B * N * sizeof(float) > x->ws_bytes) return fail(PGMI_E_ARG, "N too large for the scratch");
     gemv_res((hipStream_t)stream, B, K, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(Wt), N,
-             reinterpret_cast<uint16_t*>(h));
+             reinterpret_cast<uint16_t*>(h), x->ws);
     LAUNCHCHK();
     return 0;
 }

@@ -5,6 +5,14 @@
 
 namespace pgmi {
 
+// MFMA path for 3..16 lock-step sequences (kernels_gemv_mfma.hip)
+int gemv_mf_min_batch();
+void gemv_mf_qkv(hipStream_t s, const GemvArgs& a);
+void gemv_mf_geglu(hipStream_t s, const GemvArgs& a);
+void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o);
+int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks);
+void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws);
+
 // launch-shape overrides for measurement sweeps (tools/gemv_sweep.py)
 static int tune_variant(const char* env, int dflt) {
     const char* v = std::getenv(env);
@@ -36,6 +44,10 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
+    if (B >= gemv_mf_min_batch()) {
+        gemv_mf_qkv(s, a);
+        return;
+    }
     if (B <= 1) {
         const int cap = tune_variant("PGMI_QKV_CAP", 0);
         const int upb = tune_variant("PGMI_QKV_UPB", 0);  // > 0: contiguous slices of upb units
@@ -52,9 +64,14 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     else L_(8, 4, 1, GV_QKV);
 }
 
-void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout) {
+void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
+              float* ws) {
     GemvArgs a{};
     a.x = x; a.norm_w = nullptr; a.W = W; a.n_units = N; a.K = K; a.nb = B; a.out = h_inout;
+    if (B >= gemv_mf_min_batch() && K % 128 == 0 && ws) {
+        gemv_mf_res(s, a, ws);
+        return;
+    }
     if (K == 2048) {
         if (B <= 1) L_(1, 4, 1, GV_RES);
         else if (B <= 2) L_(2, 4, 1, GV_RES);
@@ -83,6 +100,10 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
     GemvArgs a{};
     a.x = nullptr; a.norm_w = nullptr; a.W = Wo; a.n_units = N; a.K = G * 256; a.nb = B; a.out = h_inout;
     a.part = part; a.max_chunks = max_chunks; a.G = G; a.st = st; a.o_out = o_out;
+    if (B >= gemv_mf_min_batch() && o_out) {
+        gemv_mf_ores(s, a, o_out);
+        return;
+    }
     // grid capped so each workgroup's combine prologue is amortised over 8 output rows
     if (B <= 1) {
         const int cap = tune_variant("PGMI_O_CAP", 256);
@@ -98,6 +119,10 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
                 int I, uint16_t* act) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
+    if (B >= gemv_mf_min_batch()) {
+        gemv_mf_geglu(s, a);
+        return;
+    }
     if (B <= 1) {
         const int cap = tune_variant("PGMI_GU_CAP", 1024);
         const int rpw = tune_variant("PGMI_GU_RPW", 1);
@@ -120,6 +145,10 @@ void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
     int mb = tune_variant("PGMI_LM_CAP", gemv_logits_blocks());
     if (mb < 1 || mb > gemv_logits_blocks()) mb = gemv_logits_blocks();  // pmax/pidx capacity
     int blocks;
+    if (B >= gemv_mf_min_batch()) {
+        *nparts = gemv_mf_logits(s, a, mb);
+        return;
+    }
 #define LG_(b_, rpw)                                                    \
     do {                                                                \
         blocks = (V + 4 * rpw - 1) / (4 * rpw);                         \

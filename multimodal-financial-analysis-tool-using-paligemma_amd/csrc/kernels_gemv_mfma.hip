@@ -1,0 +1,712 @@
+// kernels_gemv_mfma.hip -- decode projections for 2..16 sequences in lock-step (BASELINE configs[3]:
+// 8 images per GPU), on MFMA.
+//
+// At batch 1 a decode projection is one HBM pass with v_dot2 (gemv_body.h).  At batch B the
+// same pass owes B dot products per weight byte; on v_dot2 that turns the pass VALU-bound (B = 8:
+// gate/up 90 us vs 22 us at B = 1).  Here the batch rows are the M side of a v_mfma_f32_16x16x32_bf16
+// (rows >= B are zero) and 16 weight rows are the N side, so the pass is back to one read of
+// the weights:
+//   - one wave owns a 16-unit group (16 weight rows; 16 row pairs for RoPE / GeGLU) over a
+//     KW-wide slice of K; WK waves of a workgroup split K and meet in LDS; KS workgroups split
+//     it further for the 16384-wide down_proj (fp32 partial slabs, reduced by k_mf_combine);
+//   - B operand (weights) straight from HBM in the MFMA layout: lane (n = lane & 15, g = lane >> 4)
+//     reads 16 B of row n at k = 32i + 8g, so one load instruction covers 64 contiguous bytes of
+//     each of its 16 rows (non-temporal);
+//   - A operand (activations, B x K bf16): the wave's K slice held in registers, staged through
+//     LDS (row stride K + 8: conflict-free 16-B reads) with the RMSNorm (modeling_gemma.py:114-120)
+//     or the flash-decoding combine (o_proj) fused in, or read from global (down_proj's input);
+//   - epilogues and rounding points exactly as gemv_body.h (RoPE + KV append, GeGLU, residual,
+//     fp32 logits + per-workgroup first-max argmax partials).
+#include "gemv_body.h"
+
+#include <cstdlib>
+
+namespace pgmi {
+
+constexpr int MF_MAXB = 16;
+
+// flash-decoding combine of k_attn_decode's partials into xs rows (stride ld), fixed chunk order
+// (the GV_ORES prologue of gemv_body.h, restated for the padded LDS image)
+__device__ void mf_stage_ores(const GemvArgs& a, int K, uint16_t* xs, int ld) {
+    const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
+    for (int e8 = threadIdx.x; e8 < a.nb * K / 8; e8 += blockDim.x) {
+        const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
+        const int h = e >> 8;
+        const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + (e & 255);
+        const float* sp = a.part + (long)b * a.max_chunks * kAttnPartStride + 16 * 256 + h;
+        float M = -INFINITY, S = 0.f, o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = 0.f;
+        for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
+        for (int c = 0; c < nch; ++c) {
+            const float w = expf(sp[(long)c * kAttnPartStride] - M);
+            S += w * sp[(long)c * kAttnPartStride + 16];
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
+        }
+        u16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(o[j] / S);
+        *reinterpret_cast<u16x8*>(xs + b * ld + e) = ob;
+        if (a.o_out && blockIdx.x == 0) *reinterpret_cast<u16x8*>(a.o_out + (long)b * K + e) = ob;
+    }
+}
+
+// RMSNorm'd (or plain) activation rows into xs (stride ld).  Every row's chunks are loaded
+// before any is reduced (one round trip for the whole [nb][K] block, not one per row).
+__device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red) {
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+    float ss[MF_MAXB];
+#pragma unroll
+    for (int b = 0; b < MF_MAXB; ++b) ss[b] = 0.f;
+    for (int c = tid * 8; c < K; c += nt * 8) {  // K = 2048 with 256 threads: one pass
+        uint4 v[MF_MAXB];
+#pragma unroll
+        for (int b = 0; b < MF_MAXB; ++b)
+            if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + c);
+#pragma unroll
+        for (int b = 0; b < MF_MAXB; ++b)
+            if (b < a.nb) {
+                *reinterpret_cast<uint4*>(xs + b * ld + c) = v[b];
+                const uint16_t* e = reinterpret_cast<const uint16_t*>(&v[b]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { const float f = bf2f(e[j]); ss[b] += f * f; }
+            }
+    }
+    if (!a.norm_w) return;
+#pragma unroll
+    for (int b = 0; b < MF_MAXB; ++b)
+        if (b < a.nb) {
+            const float t = wave_sum(ss[b]);
+            if (lane == 0) red[b * 16 + wave] = t;
+        }
+    __syncthreads();
+    float r[MF_MAXB];
+#pragma unroll
+    for (int b = 0; b < MF_MAXB; ++b) {
+        float t = 0.f;
+        if (b < a.nb)
+            for (int w = 0; w < nw; ++w) t += red[b * 16 + w];  // fixed order
+        r[b] = 1.0f / sqrtf(t / (float)K + a.eps);
+    }
+    for (int c = tid * 8; c < K; c += nt * 8) {
+        const uint4 wv = ldg16(a.norm_w + c);
+        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+#pragma unroll
+        for (int b = 0; b < MF_MAXB; ++b)
+            if (b < a.nb) {
+                const uint4 v = *reinterpret_cast<const uint4*>(xs + b * ld + c);
+                const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+                u16x8 o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r[b]) * (1.0f + bf2f(we[j])));
+                *reinterpret_cast<u16x8*>(xs + b * ld + c) = o;
+            }
+    }
+}
+
+// MODE: GV_*; NR: weight rows per unit (2: RoPE / GeGLU pairs); KW: K elements per wave; WK:
+// waves per unit group (K split inside the workgroup).  grid.x: unit-group slots (grid-stride
+// over groups), grid.y: KS (K split over workgroups; GV_RES only, partials to ws).
+template <int MODE, int NR, int KW, int WK>
+__global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restrict__ ws) {
+    constexpr int NKB = KW / 128;          // 128-wide k blocks per wave
+    constexpr bool STAGE = (MODE != GV_RES);
+    extern __shared__ __attribute__((aligned(16))) uint16_t mfs[];
+    __shared__ float red[MF_MAXB * 16];
+    __shared__ f32x4 kred[WK][NR][64];
+    const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
+    const int n = lane & 15, g = lane >> 4;
+    const int K = a.K, ld = K + 8;
+    const int KS = gridDim.y, ks = blockIdx.y;
+    const int k0 = (ks * WK + wk) * KW;
+    const int n_groups = (a.n_units + 15) / 16;
+
+    auto row_of = [&](int u, int j) -> long {
+        if constexpr (MODE == GV_QKV) return (long)((u >> 7) * 256 + (u & 127) + j * 128);
+        else if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
+        else return (long)u;
+    };
+    uint4 w[NR][NKB][4];
+    auto issue = [&](int grp) {
+        int u = grp * 16 + n;
+        if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const uint16_t* rp = a.W + row_of(u, j) * K + k0 + 8 * g;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[j][kb][i] = ldg_nt(rp + kb * 128 + 32 * i);
+        }
+    };
+    int grp = blockIdx.x;
+    if (grp < n_groups) issue(grp);
+
+    // ---- activations: this wave's K slice, MFMA A layout (row b = lane & 15)
+    short8 xf[NKB][4];
+    if constexpr (STAGE) {
+        if constexpr (MODE == GV_ORES) mf_stage_ores(a, K, mfs, ld);
+        else mf_stage_rows(a, K, mfs, ld, red);
+        __syncthreads();
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xf[kb][i] = n < a.nb ? *reinterpret_cast<const short8*>(mfs + n * ld + k0 + kb * 128 + 32 * i + 8 * g)
+                                     : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xf[kb][i] = n < a.nb ? __builtin_bit_cast(short8, ldg16(a.x + (long)n * K + k0 + kb * 128 + 32 * i + 8 * g))
+                                     : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+
+    int kv_len = 0, pos = 0;
+    if constexpr (MODE == GV_QKV) {
+        kv_len = a.st->kv_len;
+        pos = a.st->position;
+        if (pos < 0) pos = 0;
+        if (pos > a.max_pos - 1) pos = a.max_pos - 1;  // clamp (modeling_gemma.py:163-165)
+    }
+    float best[4];
+    int besti[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { best[r] = -INFINITY; besti[r] = 0x7fffffff; }
+
+    for (; grp < n_groups; grp += gridDim.x) {
+        f32x4 acc[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[j] = mfma16(xf[kb][i], __builtin_bit_cast(short8, w[j][kb][i]), acc[j]);
+        }
+        const int cur = grp;
+        if (grp + gridDim.x < n_groups) issue(grp + gridDim.x);  // next group's stream starts now
+        if constexpr (WK > 1) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j) kred[wk][j][lane] = acc[j];
+            __syncthreads();
+            if (wk == 0) {
+#pragma unroll
+                for (int j = 0; j < NR; ++j) {
+                    acc[j] = kred[0][j][lane];
+#pragma unroll
+                    for (int q = 1; q < WK; ++q) acc[j] += kred[q][j][lane];
+                }
+            }
+            __syncthreads();
+            if (wk != 0) continue;
+        }
+        // C map: col n = unit (cur*16 + n), row b = 4g + r
+        const int u = cur * 16 + n;
+        if (u >= a.n_units) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = 4 * g + r;
+            if (b >= a.nb) break;
+            if constexpr (MODE == GV_RES) {
+                if (KS > 1) ws[((long)ks * a.nb + b) * a.n_units + u] = acc[0][r];
+                else a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
+            } else if constexpr (MODE == GV_ORES) {
+                a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
+            } else if constexpr (MODE == GV_GEGLU) {
+                const float gg = rbf(gelu_tanh(rbf(acc[0][r])));
+                a.out[(long)b * a.I + u] = f2bf(gg * rbf(acc[1][r]));
+            } else if constexpr (MODE == GV_LOGITS) {
+                const float v = rbf(acc[0][r]);
+                a.logits[(long)b * a.n_units + u] = v;
+                if (v > best[r]) { best[r] = v; besti[r] = u; }  // units visited in increasing order
+            } else {  // GV_QKV
+                const int hh = u >> 7, d = u & 127;
+                const float x0 = rbf(acc[0][r]), x1 = rbf(acc[1][r]);
+                const int nh = a.I;
+                if (hh < nh + a.nkv) {
+                    const float c = bf2f(a.cosT[(long)pos * 128 + d]);
+                    const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
+                    const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
+                    const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sn));
+                    uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256
+                                            : a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
+                    dst[d] = o0;
+                    dst[d + 128] = o1;
+                } else {
+                    uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh - a.nkv) * 256;
+                    dst[d] = f2bf(x0);
+                    dst[d + 128] = f2bf(x1);
+                }
+            }
+        }
+    }
+    if constexpr (MODE == GV_LOGITS) {
+        // first max per batch row over this workgroup's units: lanes of one g hold 16 columns
+        __shared__ float bv[MF_MAXB];
+        __shared__ int bi[MF_MAXB];
+        if (wk == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float m = best[r];
+                int mi = besti[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const float m2 = __shfl_xor(m, o, 64);
+                    const int i2 = __shfl_xor(mi, o, 64);
+                    if (m2 > m || (m2 == m && i2 < mi)) { m = m2; mi = i2; }
+                }
+                if (n == 0) { bv[4 * g + r] = m; bi[4 * g + r] = mi; }
+            }
+        }
+        __syncthreads();
+        if (tid < a.nb) {
+            a.pmax[(long)tid * gridDim.x + blockIdx.x] = bv[tid];
+            a.pidx[(long)tid * gridDim.x + blockIdx.x] = bi[tid];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- streaming form
+// One wave streams whole 16-row groups over a KSL-wide K slice with D 128-wide k blocks in
+// flight (the B=1 GEMV's access pattern, MFMA instead of v_dot2), groups dealt grid-stride to
+// the 4 waves of each workgroup; the workgroup stages its K slice of the activation rows in LDS
+// once (RMSNorm fused when the slice is the whole row) and every MFMA reads its A fragment
+// there.  grid.y = K slices (GV_RES only: fp32 partials to ws, reduced by k_mf_combine).
+template <int MODE, int NR, int KSL, int D>
+__global__ void __launch_bounds__(256) k_gemv_ms(GemvArgs a, float* __restrict__ ws) {
+    constexpr int NKB = KSL / 128;
+    static_assert(NKB % D == 0, "k blocks per slice must be a multiple of the pipeline depth");
+    extern __shared__ __attribute__((aligned(16))) uint16_t mss[];
+    __shared__ float red[MF_MAXB * 16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = lane & 15, g = lane >> 4;
+    const int K = a.K, ld = KSL + 8;
+    const int KS = gridDim.y, ks = blockIdx.y;
+    const int k0 = ks * KSL;
+    const int n_groups = (a.n_units + 15) / 16;
+    const int gstride = gridDim.x * 4;
+
+    auto row_of = [&](int u, int j) -> long {
+        if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
+        else return (long)u;
+    };
+    uint4 w[D][NR][4];
+    auto issue = [&](int grp, int kb, int slot) {
+        int u = grp * 16 + n;
+        if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const uint16_t* rp = a.W + row_of(u, j) * K + k0 + kb * 128 + 8 * g;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[slot][j][i] = ldg16(rp + 32 * i);
+        }
+    };
+    int grp = blockIdx.x * 4 + wave;
+    if (grp < n_groups) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) issue(grp, d, d);
+    }
+    // stage x[:, k0 : k0 + KSL] (rows < nb) in LDS; the whole row carries the RMSNorm
+    if (a.norm_w) {
+        mf_stage_rows(a, K, mss, ld, red);
+    } else {
+        for (int c = tid * 8; c < KSL; c += 256 * 8) {  // all rows' chunks in one round trip
+            uint4 v[MF_MAXB];
+#pragma unroll
+            for (int b = 0; b < MF_MAXB; ++b)
+                if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + k0 + c);
+#pragma unroll
+            for (int b = 0; b < MF_MAXB; ++b)
+                if (b < a.nb) *reinterpret_cast<uint4*>(mss + b * ld + c) = v[b];
+        }
+    }
+    __syncthreads();
+    const int xrow = n < a.nb ? n : 0;  // rows >= nb: read row 0, zeroed below
+    const uint16_t* xa = mss + xrow * ld + 8 * g;
+    const bool xz = n >= a.nb;
+
+    float best[4];
+    int besti[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { best[r] = -INFINITY; besti[r] = 0x7fffffff; }
+
+    for (; grp < n_groups; grp += gstride) {
+        const int nxt = grp + gstride;
+        f32x4 acc[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const int slot = kb % D;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                short8 xv = *reinterpret_cast<const short8*>(xa + kb * 128 + 32 * i);
+                if (xz) xv = short8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < NR; ++j) acc[j] = mfma16(xv, __builtin_bit_cast(short8, w[slot][j][i]), acc[j]);
+            }
+            // refill the slot: block kb + D of this group, or the head of the next group
+            if (kb + D < NKB) issue(grp, kb + D, slot);
+            else if (nxt < n_groups) issue(nxt, kb + D - NKB, slot);
+        }
+        const int u = grp * 16 + n;
+        if (u >= a.n_units) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = 4 * g + r;
+            if (b >= a.nb) break;
+            if constexpr (MODE == GV_RES) {
+                if (KS > 1) ws[((long)ks * a.nb + b) * a.n_units + u] = acc[0][r];
+                else a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
+            } else if constexpr (MODE == GV_GEGLU) {
+                const float gg = rbf(gelu_tanh(rbf(acc[0][r])));
+                a.out[(long)b * a.I + u] = f2bf(gg * rbf(acc[1][r]));
+            } else {  // GV_LOGITS
+                const float v = rbf(acc[0][r]);
+                a.logits[(long)b * a.n_units + u] = v;
+                if (v > best[r]) { best[r] = v; besti[r] = u; }  // units visited in increasing order
+            }
+        }
+    }
+    if constexpr (MODE == GV_LOGITS) {
+        __shared__ float bv[4][MF_MAXB];
+        __shared__ int bi[4][MF_MAXB];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float m = best[r];
+            int mi = besti[r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const float m2 = __shfl_xor(m, o, 64);
+                const int i2 = __shfl_xor(mi, o, 64);
+                if (m2 > m || (m2 == m && i2 < mi)) { m = m2; mi = i2; }
+            }
+            if (n == 0) { bv[wave][4 * g + r] = m; bi[wave][4 * g + r] = mi; }
+        }
+        __syncthreads();
+        if (tid < a.nb) {
+            float m = bv[0][tid];
+            int mi = bi[0][tid];
+            for (int q = 1; q < 4; ++q)
+                if (bv[q][tid] > m || (bv[q][tid] == m && bi[q][tid] < mi)) { m = bv[q][tid]; mi = bi[q][tid]; }
+            a.pmax[(long)tid * gridDim.x + blockIdx.x] = m;
+            a.pidx[(long)tid * gridDim.x + blockIdx.x] = mi;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- LDS-DMA streaming form
+// As k_gemv_ms, but the weights reach the MFMA through a per-wave LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4): one instruction moves 4 whole 256-B row segments (1 KiB,
+// coalesced), where the MFMA-layout register loads touch 16 rows x 64 B each.  Row r's 16-B
+// chunk c lands at chunk (c ^ (r & 15)) of its 256-B LDS row (applied to each lane's SOURCE
+// address, the LDS-DMA destination being lane-linear), so the B-fragment ds_read_b128s of 16
+// rows x one 16-B k slice are conflict-free.  Each wave owns its ring: completion is its own
+// vmcnt, no barrier.
+template <int N>
+__device__ __forceinline__ void mf_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int NR, int KSL, int D>
+__global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restrict__ ws) {
+    constexpr int NKB = KSL / 128;
+    constexpr int SLOT = NR * 16 * 256;  // bytes of one k block of the wave's rows
+    constexpr int PER = NR * 4;          // LDS-DMA instructions per k block
+    static_assert((D - 1) * PER <= 63, "ring shape");
+    extern __shared__ __attribute__((aligned(16))) uint8_t mls[];
+    __shared__ float red[MF_MAXB * 16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = lane & 15, g = lane >> 4;
+    const int K = a.K, ld = KSL + 8;
+    const int KS = gridDim.y, ks = blockIdx.y;
+    const int k0 = ks * KSL;
+    const int n_groups = (a.n_units + 15) / 16;
+    const int gstride = gridDim.x * 4;
+    uint16_t* xs = reinterpret_cast<uint16_t*>(mls);
+    uint8_t* ring = mls + (((size_t)a.nb * ld * 2 + 127) & ~(size_t)127) + (size_t)wave * D * SLOT;
+
+    auto row_of = [&](int u, int j) -> long {
+        if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
+        else return (long)u;
+    };
+    // LDS-DMA of k block kb of group grp into slot: instruction q (of PER) covers rows
+    // 4(q % 4) .. +3 of row set j = q / 4; lane -> row 4(q%4) + (lane >> 4), position lane & 15
+    const int prow = lane >> 4, ppos = lane & 15;
+    auto issue = [&](int grp, int kb, int slot) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int j = q / 4, r = 4 * (q % 4) + prow;
+            int u = grp * 16 + r;
+            if (u >= a.n_units) u = a.n_units - 1;
+            const int c = ppos ^ r;  // source chunk landing at position ppos of row r
+            const uint16_t* src = a.W + row_of(u, j) * K + k0 + kb * 128 + c * 8;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                             (__attribute__((address_space(3))) void*)(ring + slot * SLOT + q * 1024), 16, 0, 0);
+        }
+    };
+    int grp = blockIdx.x * 4 + wave;
+    // activations first (their loads must not sit between the ring's counted LDS-DMAs)
+    if (a.norm_w) {
+        mf_stage_rows(a, K, xs, ld, red);
+    } else {
+        for (int c = tid * 8; c < KSL; c += 256 * 8) {
+            uint4 v[MF_MAXB];
+#pragma unroll
+            for (int b = 0; b < MF_MAXB; ++b)
+                if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + k0 + c);
+#pragma unroll
+            for (int b = 0; b < MF_MAXB; ++b)
+                if (b < a.nb) *reinterpret_cast<uint4*>(xs + b * ld + c) = v[b];
+        }
+    }
+    __syncthreads();
+    mf_vmcnt<0>();
+    if (grp < n_groups) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) issue(grp, d, d);
+    }
+    const int xrow = n < a.nb ? n : 0;
+    const uint16_t* xa = xs + xrow * ld + 8 * g;
+    const bool xz = n >= a.nb;
+    int slot0 = 0;  // ring slot of this group's block 0 (the stream runs on across groups)
+
+    float best[4];
+    int besti[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { best[r] = -INFINITY; besti[r] = 0x7fffffff; }
+
+    for (; grp < n_groups; grp += gstride) {
+        const int nxt = grp + gstride;
+        const bool more = nxt < n_groups;
+        f32x4 acc[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const int slot = (slot0 + kb) % D;
+            // block kb landed: the younger D-1 blocks may still be in flight (only while they exist)
+            if (kb + D <= NKB || more) mf_vmcnt<(D - 1) * PER>();
+            else mf_vmcnt<0>();
+            const uint8_t* sb = ring + slot * SLOT + n * 256;
+            short8 wf[NR][4];
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    wf[j][i] = *reinterpret_cast<const short8*>(sb + j * 4096 + (((4 * i + g) ^ n) << 4));
+            short8 xv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xv[i] = *reinterpret_cast<const short8*>(xa + kb * 128 + 32 * i);
+                if (xz) xv[i] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot's reads are done
+            if (kb + D < NKB) issue(grp, kb + D, slot);
+            else if (more) issue(nxt, kb + D - NKB, slot);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < NR; ++j) acc[j] = mfma16(xv[i], wf[j][i], acc[j]);
+        }
+        slot0 = (slot0 + NKB) % D;
+        const int u = grp * 16 + n;
+        if (u >= a.n_units) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = 4 * g + r;
+            if (b >= a.nb) break;
+            if constexpr (MODE == GV_RES) {
+                if (KS > 1) ws[((long)ks * a.nb + b) * a.n_units + u] = acc[0][r];
+                else a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
+            } else if constexpr (MODE == GV_GEGLU) {
+                const float gg = rbf(gelu_tanh(rbf(acc[0][r])));
+                a.out[(long)b * a.I + u] = f2bf(gg * rbf(acc[1][r]));
+            } else {  // GV_LOGITS
+                const float v = rbf(acc[0][r]);
+                a.logits[(long)b * a.n_units + u] = v;
+                if (v > best[r]) { best[r] = v; besti[r] = u; }
+            }
+        }
+    }
+    if constexpr (MODE == GV_LOGITS) {
+        __shared__ float bv[4][MF_MAXB];
+        __shared__ int bi[4][MF_MAXB];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float m = best[r];
+            int mi = besti[r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const float m2 = __shfl_xor(m, o, 64);
+                const int i2 = __shfl_xor(mi, o, 64);
+                if (m2 > m || (m2 == m && i2 < mi)) { m = m2; mi = i2; }
+            }
+            if (n == 0) { bv[wave][4 * g + r] = m; bi[wave][4 * g + r] = mi; }
+        }
+        __syncthreads();
+        if (tid < a.nb) {
+            float m = bv[0][tid];
+            int mi = bi[0][tid];
+            for (int q = 1; q < 4; ++q)
+                if (bv[q][tid] > m || (bv[q][tid] == m && bi[q][tid] < mi)) { m = bv[q][tid]; mi = bi[q][tid]; }
+            a.pmax[(long)tid * gridDim.x + blockIdx.x] = m;
+            a.pidx[(long)tid * gridDim.x + blockIdx.x] = mi;
+        }
+    }
+}
+
+// flash-decoding combine of k_attn_decode's partials -> o (bf16 [nb][G*256]), one thread per
+// 8 outputs, chunk records in a fixed order (the GV_ORES prologue, once per output)
+__global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __restrict__ o, int K) {
+    const int e8 = blockIdx.x * 256 + threadIdx.x;
+    if (e8 >= a.nb * K / 8) return;
+    const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
+    const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
+    const int h = e >> 8;
+    const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + (e & 255);
+    const float* sp = a.part + (long)b * a.max_chunks * kAttnPartStride + 16 * 256 + h;
+    float M = -INFINITY, S = 0.f, acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
+    for (int c = 0; c < nch; ++c) {
+        const float wgt = expf(sp[(long)c * kAttnPartStride] - M);
+        S += wgt * sp[(long)c * kAttnPartStride + 16];
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[j] += wgt * x0[j]; acc[4 + j] += wgt * x1[j]; }
+    }
+    u16x8 ob;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(acc[j] / S);
+    *reinterpret_cast<u16x8*>(o + (long)b * K + e) = ob;
+}
+
+// h[b][n] = bf16(bf16(sum_ks ws[ks][b][n]) + h[b][n]), fixed ks order
+__global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N, uint16_t* __restrict__ h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nb * N) return;
+    float s = ws[i];
+    for (int q = 1; q < KS; ++q) s += ws[(long)q * nb * N + i];
+    h[i] = f2bf(rbf(s) + bf2f(h[i]));
+}
+
+// launch-shape override for measurement (tools/probes): PGMI_MF_MINB = smallest batch on MFMA
+int gemv_mf_min_batch() {
+    static const int v = [] {
+        const char* e = std::getenv("PGMI_MF_MINB");
+        return e ? std::atoi(e) : 3;
+    }();
+    return v;
+}
+
+template <int MODE, int NR, int KW, int WK>
+static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
+    const size_t lds = (MODE == GV_RES) ? 0 : (size_t)a.nb * (a.K + 8) * sizeof(uint16_t);
+    static size_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = lds;
+    }
+    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
+}
+
+static int groups_of(int units) { return (units + 15) / 16; }
+
+void gemv_mf_qkv(hipStream_t s, const GemvArgs& a) {  // K = 2048: 8 waves x 256
+    launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
+}
+
+template <int MODE, int NR, int KSL, int D>
+static void launch_ms(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
+    const size_t lds = (size_t)a.nb * (KSL + 8) * sizeof(uint16_t);
+    static size_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_ms<MODE, NR, KSL, D>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = lds;
+    }
+    hipLaunchKernelGGL((k_gemv_ms<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(256), lds, s, a, ws);
+}
+
+template <int MODE, int NR, int KSL, int D>
+static void launch_ml(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
+    const size_t lds = (((size_t)a.nb * (KSL + 8) * 2 + 127) & ~(size_t)127) + (size_t)4 * D * NR * 16 * 256;
+    static size_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_ml<MODE, NR, KSL, D>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = lds;
+    }
+    hipLaunchKernelGGL((k_gemv_ml<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(256), lds, s, a, ws);
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
+// workgroups of 4 streaming waves: every group once, capped at `cap` workgroups (grid-stride)
+static int ms_blocks(int units, int cap) {
+    const int wg = (groups_of(units) + 3) / 4;
+    return wg < cap ? wg : cap;
+}
+
+void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
+    if (env_int("PGMI_MF_ML", 1)) launch_ml<GV_GEGLU, 2, 2048, 3>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
+    else launch_ms<GV_GEGLU, 2, 2048, 4>(s, a, ms_blocks(a.n_units, env_int("PGMI_MF_GU_CAP", 512)), 1, nullptr);
+}
+
+// o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
+void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
+    const int K = a.K;
+    hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 255) / 256), dim3(256), 0, s, a, o, K);
+    GemvArgs r = a;
+    r.x = o;
+    r.norm_w = nullptr;
+    if (env_int("PGMI_MF_ML", 1)) launch_ml<GV_RES, 1, 2048, 6>(s, r, ms_blocks(a.n_units, 256), 1, nullptr);
+    else launch_ms<GV_RES, 1, 2048, 4>(s, r, ms_blocks(a.n_units, 1024), 1, nullptr);
+}
+
+int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2048
+    if (env_int("PGMI_MF_ML", 1)) {
+        const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
+        launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
+        return blocks;
+    }
+    const int blocks = ms_blocks(a.n_units, max_blocks < 1024 ? max_blocks : 1024);
+    launch_ms<GV_LOGITS, 1, 2048, 4>(s, a, blocks, 1, nullptr);
+    return blocks;
+}
+
+// residual projections; ws: fp32 scratch of KS x nb x N floats for the K split of K = 16384
+void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws) {
+    const bool ml = env_int("PGMI_MF_ML", 1) != 0;
+    if (a.K == 2048) {
+        if (ml) launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
+        else launch_ms<GV_RES, 1, 2048, 4>(s, a, ms_blocks(a.n_units, 1024), 1, nullptr);
+        return;
+    }
+    if (a.K % 2048 == 0 && ws) {  // K slices of 2048 over grid.y, fp32 partials, fixed-order combine
+        const int KS = a.K / 2048;
+        if (ml) launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), KS, ws);
+        else launch_ms<GV_RES, 1, 2048, 4>(s, a, ms_blocks(a.n_units, 1024), KS, ws);
+        const int nn = a.nb * a.n_units;
+        hipLaunchKernelGGL(k_mf_combine, dim3((nn + 255) / 256), dim3(256), 0, s, ws, KS, a.nb, a.n_units, a.out);
+        return;
+    }
+    const int G = groups_of(a.n_units);
+    launch_mf<GV_RES, 1, 128, 1>(s, a, G, a.K / 128, ws);  // generic K (multiple of 128)
+    const int nn = a.nb * a.n_units;
+    hipLaunchKernelGGL(k_mf_combine, dim3((nn + 255) / 256), dim3(256), 0, s, ws, a.K / 128, a.nb, a.n_units, a.out);
+}
+
+}  // namespace pgmi

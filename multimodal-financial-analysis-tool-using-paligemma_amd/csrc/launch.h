@@ -48,7 +48,9 @@ struct StepState {  // device-resident decode step (read by kernels -> graph-rep
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
               uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride);
-void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout);
+// ws: fp32 scratch (>= 4 x B x N floats) for the MFMA path's K split of K = 16384 (B >= 3)
+void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
+              float* ws);
 // o_proj + residual whose input is the combine of the decode-attention partials (MQA:
 // n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
@@ -56,6 +58,7 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                 const uint16_t* Wgu, int I, uint16_t* act);
 int gemv_logits_blocks();
+int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts);
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out);

@@ -968,8 +968,13 @@ int pgmi_sample_top_p(pgmi_ctx* x, const float* logits, int rows, int V, float t
     if (rows <= 0 || V <= 0) return fail(PGMI_E_ARG, "sample_top_p: empty probabilities");
     if (!(top_p >= 0.f)) return fail(PGMI_E_ARG, "sample_top_p: top_p must be >= 0");
     if (!x->ws) return fail(PGMI_E_STATE, "workspace not allocated (pgmi_prepare)");
-    if ((size_t)rows * V * sizeof(float) > x->ws_bytes) return fail(PGMI_E_ARG, "sample_top_p: rows x vocab exceed the scratch");
-    sample_top_p((hipStream_t)stream, logits, rows, V, temperature, top_p, u, x->ws, out, kept_mass);
+    const int per = (int)std::min<size_t>((size_t)rows, x->ws_bytes / sample_scratch_bytes(1, V));
+    if (per < 1) return fail(PGMI_E_ARG, "sample_top_p: vocabulary exceeds the scratch");
+    for (int r0 = 0; r0 < rows; r0 += per) {  // row batches that fit the scratch (stream-ordered)
+        const int nr = std::min(per, rows - r0);
+        sample_top_p((hipStream_t)stream, logits + (size_t)r0 * V, nr, V, temperature, top_p, u + r0, x->ws,
+                     out + r0, kept_mass ? kept_mass + r0 : nullptr);
+    }
     LAUNCHCHK();
     return 0;
 }

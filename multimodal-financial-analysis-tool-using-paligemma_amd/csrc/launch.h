@@ -119,9 +119,10 @@ void set_step(hipStream_t s, StepState* st, int kv_len, int position);
 size_t preprocess_scratch_bytes(int H, int W, int out_h, int out_w);
 void preprocess(hipStream_t s, const uint8_t* src, int H, int W, int out_h, int out_w, float* out, void* scratch);
 void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uint16_t* dst);
-// nucleus sampling (kernels_sample.hip; inference.py:15-24, :65): scratch = rows x V fp32
+// nucleus sampling (kernels_sample.hip; inference.py:15-24, :65); scratch of sample_scratch_bytes()
+size_t sample_scratch_bytes(int rows, int V);
 void sample_top_p(hipStream_t s, const float* x, int rows, int V, float temperature, float top_p, const float* u,
-                  float* scratch, int64_t* out, float* kept_mass);
+                  void* scratch, int64_t* out, float* kept_mass);
 
 
 // ---- fused decode step (kernels_step.hip): batch 1, one launch per token

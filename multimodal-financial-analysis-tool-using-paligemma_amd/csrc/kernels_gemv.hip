@@ -7,7 +7,7 @@ namespace pgmi {
 
 // MFMA path for 3..16 lock-step sequences (kernels_gemv_mfma.hip)
 int gemv_mf_min_batch();
-void gemv_mf_qkv(hipStream_t s, const GemvArgs& a);
+void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* ws);
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a);
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o);
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks);
@@ -38,14 +38,14 @@ static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
 // K = 2048 (hidden); nh q heads, nkv kv heads of 256
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
-              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride) {
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wqkv; a.n_units = (nh + 2 * nkv) * 128; a.K = 2048; a.nb = B;
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
     if (B >= gemv_mf_min_batch()) {
-        gemv_mf_qkv(s, a);
+        gemv_mf_qkv(s, a, ws);
         return;
     }
     if (B <= 1) {

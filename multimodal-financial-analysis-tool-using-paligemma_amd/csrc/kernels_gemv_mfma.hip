@@ -56,20 +56,24 @@ __device__ void mf_stage_ores(const GemvArgs& a, int K, uint16_t* xs, int ld) {
 
 // RMSNorm'd (or plain) activation rows into xs (stride ld).  Every row's chunks are loaded
 // before any is reduced (one round trip for the whole [nb][K] block, not one per row).
-__device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red) {
+__device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red, int k0 = 0, int ksl = -1) {
+    if (ksl < 0) ksl = K;  // stage columns [k0, k0 + ksl) at xs column 0; the norm uses the whole row
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
     float ss[MF_MAXB];
 #pragma unroll
     for (int b = 0; b < MF_MAXB; ++b) ss[b] = 0.f;
-    for (int c = tid * 8; c < K; c += nt * 8) {  // K = 2048 with 256 threads: one pass
+    const bool one = (K == nt * 8);  // K = 2048, 256 threads: one chunk per thread, norm weights fetched now
+    const uint4 wv0 = (one && a.norm_w) ? ldg16(a.norm_w + tid * 8) : make_uint4(0, 0, 0, 0);
+    for (int c = tid * 8; c < K; c += nt * 8) {
         uint4 v[MF_MAXB];
 #pragma unroll
-        for (int b = 0; b < MF_MAXB; ++b)
-            if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + c);
+        for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): the loads stay in flight together
+            v[b] = ldg16(a.x + (long)(b < a.nb ? b : a.nb - 1) * K + c);
+        const bool mine = c >= k0 && c < k0 + ksl;
 #pragma unroll
         for (int b = 0; b < MF_MAXB; ++b)
             if (b < a.nb) {
-                *reinterpret_cast<uint4*>(xs + b * ld + c) = v[b];
+                if (mine) *reinterpret_cast<uint4*>(xs + b * ld + (c - k0)) = v[b];
                 const uint16_t* e = reinterpret_cast<const uint16_t*>(&v[b]);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { const float f = bf2f(e[j]); ss[b] += f * f; }
@@ -91,18 +95,19 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
             for (int w = 0; w < nw; ++w) t += red[b * 16 + w];  // fixed order
         r[b] = 1.0f / sqrtf(t / (float)K + a.eps);
     }
-    for (int c = tid * 8; c < K; c += nt * 8) {
-        const uint4 wv = ldg16(a.norm_w + c);
+    for (int c = one ? tid * 8 : k0 + tid * 8; c < k0 + ksl; c += nt * 8) {
+        if (c < k0) continue;
+        const uint4 wv = one ? wv0 : ldg16(a.norm_w + c);
         const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
 #pragma unroll
         for (int b = 0; b < MF_MAXB; ++b)
             if (b < a.nb) {
-                const uint4 v = *reinterpret_cast<const uint4*>(xs + b * ld + c);
+                const uint4 v = *reinterpret_cast<const uint4*>(xs + b * ld + (c - k0));
                 const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
                 u16x8 o;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r[b]) * (1.0f + bf2f(we[j])));
-                *reinterpret_cast<u16x8*>(xs + b * ld + c) = o;
+                *reinterpret_cast<u16x8*>(xs + b * ld + (c - k0)) = o;
             }
     }
 }
@@ -296,7 +301,10 @@ __global__ void __launch_bounds__(256) k_gemv_ms(GemvArgs a, float* __restrict__
         else return (long)u;
     };
     uint4 w[D][NR][4];
+    auto rot_of = [&](int grp) { return grp % NKB; };  // k-block order rotated per group (see k_gemv_ml)
     auto issue = [&](int grp, int kb, int slot) {
+        kb += rot_of(grp);
+        if (kb >= NKB) kb -= NKB;
         int u = grp * 16 + n;
         if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
 #pragma unroll
@@ -318,8 +326,8 @@ __global__ void __launch_bounds__(256) k_gemv_ms(GemvArgs a, float* __restrict__
         for (int c = tid * 8; c < KSL; c += 256 * 8) {  // all rows' chunks in one round trip
             uint4 v[MF_MAXB];
 #pragma unroll
-            for (int b = 0; b < MF_MAXB; ++b)
-                if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + k0 + c);
+            for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): one round trip
+                v[b] = ldg16(a.x + (long)(b < a.nb ? b : a.nb - 1) * K + k0 + c);
 #pragma unroll
             for (int b = 0; b < MF_MAXB; ++b)
                 if (b < a.nb) *reinterpret_cast<uint4*>(mss + b * ld + c) = v[b];
@@ -337,15 +345,17 @@ __global__ void __launch_bounds__(256) k_gemv_ms(GemvArgs a, float* __restrict__
 
     for (; grp < n_groups; grp += gstride) {
         const int nxt = grp + gstride;
+        const int rot = rot_of(grp);
         f32x4 acc[NR];
 #pragma unroll
         for (int j = 0; j < NR; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) {
             const int slot = kb % D;
+            const int kr = kb + rot < NKB ? kb + rot : kb + rot - NKB;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                short8 xv = *reinterpret_cast<const short8*>(xa + kb * 128 + 32 * i);
+                short8 xv = *reinterpret_cast<const short8*>(xa + kr * 128 + 32 * i);
                 if (xz) xv = short8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < NR; ++j) acc[j] = mfma16(xv, __builtin_bit_cast(short8, w[slot][j][i]), acc[j]);
@@ -438,7 +448,12 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
     // LDS-DMA of k block kb of group grp into slot: instruction q (of PER) covers rows
     // 4(q % 4) .. +3 of row set j = q / 4; lane -> row 4(q%4) + (lane >> 4), position lane & 15
     const int prow = lane >> 4, ppos = lane & 15;
+    // k-block order rotated per group (rot = group % NKB): concurrent waves read different
+    // offsets of their rows instead of all streaming the same 256-B column of rows 4 KiB apart
+    auto rot_of = [&](int grp) { return grp % NKB; };
     auto issue = [&](int grp, int kb, int slot) {
+        kb += rot_of(grp);
+        if (kb >= NKB) kb -= NKB;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int j = q / 4, r = 4 * (q % 4) + prow;
@@ -451,26 +466,28 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
         }
     };
     int grp = blockIdx.x * 4 + wave;
-    // activations first (their loads must not sit between the ring's counted LDS-DMAs)
+    // the ring's first D blocks go out before the activation staging: the two round trips
+    // overlap (the staging's own waits drain the ring too, so the main loop starts with every
+    // counted LDS-DMA retired)
+    if (grp < n_groups) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) issue(grp, d, d);
+    }
     if (a.norm_w) {
-        mf_stage_rows(a, K, xs, ld, red);
+        mf_stage_rows(a, K, xs, ld, red, k0, KSL);
     } else {
         for (int c = tid * 8; c < KSL; c += 256 * 8) {
             uint4 v[MF_MAXB];
 #pragma unroll
-            for (int b = 0; b < MF_MAXB; ++b)
-                if (b < a.nb) v[b] = ldg16(a.x + (long)b * K + k0 + c);
+            for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): one round trip
+                v[b] = ldg16(a.x + (long)(b < a.nb ? b : a.nb - 1) * K + k0 + c);
 #pragma unroll
             for (int b = 0; b < MF_MAXB; ++b)
                 if (b < a.nb) *reinterpret_cast<uint4*>(xs + b * ld + c) = v[b];
         }
     }
-    __syncthreads();
     mf_vmcnt<0>();
-    if (grp < n_groups) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) issue(grp, d, d);
-    }
+    __syncthreads();
     const int xrow = n < a.nb ? n : 0;
     const uint16_t* xa = xs + xrow * ld + 8 * g;
     const bool xz = n >= a.nb;
@@ -484,6 +501,7 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
     for (; grp < n_groups; grp += gstride) {
         const int nxt = grp + gstride;
         const bool more = nxt < n_groups;
+        const int rot = rot_of(grp);
         f32x4 acc[NR];
 #pragma unroll
         for (int j = 0; j < NR; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -501,9 +519,10 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
                 for (int i = 0; i < 4; ++i)
                     wf[j][i] = *reinterpret_cast<const short8*>(sb + j * 4096 + (((4 * i + g) ^ n) << 4));
             short8 xv[4];
+            const int kr = kb + rot < NKB ? kb + rot : kb + rot - NKB;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                xv[i] = *reinterpret_cast<const short8*>(xa + kb * 128 + 32 * i);
+                xv[i] = *reinterpret_cast<const short8*>(xa + kr * 128 + 32 * i);
                 if (xz) xv[i] = short8{0, 0, 0, 0, 0, 0, 0, 0};
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot's reads are done
@@ -589,6 +608,41 @@ __global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __re
     *reinterpret_cast<u16x8*>(o + (long)b * K + e) = ob;
 }
 
+// q|k|v rows from KS fp32 partial slabs ws[ks][nb][rows] (fixed ks order), then RoPE on q and k
+// and the KV-cache append (the GV_QKV epilogue of gemv_body.h, modeling_gemma.py:197-198,259):
+// one thread per (b, rotary pair (d, d + 128) of a head)
+__global__ void k_mf_qkv_rope(const float* __restrict__ ws, int KS, GemvArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int rows = (a.I + 2 * a.nkv) * 256;
+    if (i >= a.nb * (rows / 2)) return;
+    const int b = i / (rows / 2), pu = i % (rows / 2);
+    const int hh = pu >> 7, d = pu & 127;
+    const long r0 = (long)hh * 256 + d;
+    float s0 = 0.f, s1 = 0.f;
+    for (int q = 0; q < KS; ++q) {
+        s0 += ws[((long)q * a.nb + b) * rows + r0];
+        s1 += ws[((long)q * a.nb + b) * rows + r0 + 128];
+    }
+    const float x0 = rbf(s0), x1 = rbf(s1);
+    const int kv_len = a.st->kv_len;
+    int pos = a.st->position;
+    if (pos < 0) pos = 0;
+    if (pos > a.max_pos - 1) pos = a.max_pos - 1;  // clamp (modeling_gemma.py:163-165)
+    const int nh = a.I;
+    if (hh < nh + a.nkv) {
+        const float c = bf2f(a.cosT[(long)pos * 128 + d]);
+        const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
+        uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256
+                                : a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
+        dst[d] = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
+        dst[d + 128] = f2bf(rbf(x1 * c) + rbf(x0 * sn));
+    } else {
+        uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh - a.nkv) * 256;
+        dst[d] = f2bf(x0);
+        dst[d + 128] = f2bf(x1);
+    }
+}
+
 // h[b][n] = bf16(bf16(sum_ks ws[ks][b][n]) + h[b][n]), fixed ks order
 __global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N, uint16_t* __restrict__ h) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -621,9 +675,6 @@ static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, floa
 
 static int groups_of(int units) { return (units + 15) / 16; }
 
-void gemv_mf_qkv(hipStream_t s, const GemvArgs& a) {  // K = 2048: 8 waves x 256
-    launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
-}
 
 template <int MODE, int NR, int KSL, int D>
 static void launch_ms(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
@@ -658,6 +709,21 @@ static int env_int(const char* name, int dflt) {
 static int ms_blocks(int units, int cap) {
     const int wg = (groups_of(units) + 3) / 4;
     return wg < cap ? wg : cap;
+}
+
+// q|k|v: 2560 plain rows streamed over 4 K slices of 512 (320 waves where 80 row-pair groups
+// would leave most CUs idle), fp32 partials in ws, then RoPE + KV append in k_mf_qkv_rope
+void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* ws) {
+    if (!ws || env_int("PGMI_MF_QKV_SPLIT", 0) == 0) {  // default: the in-workgroup K split form (measured faster)
+        launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
+        return;
+    }
+    constexpr int KS = 4;
+    GemvArgs r = a;
+    r.n_units = (a.I + 2 * a.nkv) * 256;  // weight rows
+    launch_ml<GV_RES, 1, 512, 6>(s, r, ms_blocks(r.n_units, 256), KS, ws);
+    const int n = a.nb * r.n_units / 2;
+    hipLaunchKernelGGL(k_mf_qkv_rope, dim3((n + 255) / 256), dim3(256), 0, s, ws, KS, a);
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs

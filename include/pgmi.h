@@ -73,6 +73,19 @@ int pgmi_bind_weights(pgmi_ctx* ctx, void* dev_slab);
  * (and converts to bf16) from host or device memory into the slab. */
 int pgmi_load_weight(pgmi_ctx* ctx, const char* name, const void* src, int src_dtype, int src_on_device,
                      void* stream);
+/* Native safetensors reader (replaces the safe_open / accelerate
+ * shard loop of utils.py:19-44 and ablation_study_fixed.py:304-332): one *.safetensors file is
+ * memory-mapped and every tensor whose name is a slab weight is shape-checked, converted to bf16
+ * (BF16 copied, F32/F16 rounded to nearest even on the device) and written into the slab.
+ * Names that are not slab weights (e.g. a tied lm_head) are counted in *n_skipped.  Synchronises
+ * `stream`; call pgmi_prepare again afterwards.  A malformed header or a shape / dtype mismatch
+ * is PGMI_E_ARG (ValueError). */
+int pgmi_load_safetensors(pgmi_ctx* ctx, const char* path, int* n_loaded, int* n_skipped, void* stream);
+/* header inspection, no device needed: tensor count, and entry i's name (NUL-terminated, at most
+ * name_cap bytes), dtype (PGMI_DTYPE_*, -1 for other dtypes), shape, data byte range */
+int pgmi_safetensors_count(const char* path, int* n);
+int pgmi_safetensors_entry(const char* path, int i, char* name, int name_cap, int* dtype, int64_t* shape4, int* ndim,
+                           int64_t* begin, int64_t* end);
 /* deterministic synthetic weights (benchmarks; oracle/wgen.c recipe) */
 int pgmi_fill_synthetic(pgmi_ctx* ctx, const char* name, uint64_t key, float scale, float offset, void* stream);
 uint64_t pgmi_synthetic_key(const char* name, uint64_t seed);

@@ -19,6 +19,7 @@
 #include "../../include/pgmi.h"
 #include "common.h"
 #include "launch.h"
+#include "safetensors_hdr.h"
 
 using namespace pgmi;
 
@@ -361,6 +362,114 @@ int pgmi_load_weight(pgmi_ctx* x, const char* name, const void* src, int dtype, 
     } else {
         return fail(PGMI_E_ARG, "unsupported dtype");
     }
+    return 0;
+}
+
+int pgmi_safetensors_count(const char* path, int* n) {
+    if (!path || !n) return fail(PGMI_E_ARG, "null argument");
+    StFile f;
+    if (!st_open(path, f)) return fail(PGMI_E_ARG, f.error);
+    *n = (int)f.entries.size();
+    return 0;
+}
+
+int pgmi_safetensors_entry(const char* path, int i, char* name, int name_cap, int* dtype, int64_t* shape4, int* ndim,
+                           int64_t* begin, int64_t* end) {
+    if (!path || !name || name_cap < 1 || !dtype || !shape4 || !ndim || !begin || !end)
+        return fail(PGMI_E_ARG, "null argument");
+    StFile f;
+    if (!st_open(path, f)) return fail(PGMI_E_ARG, f.error);
+    if (i < 0 || i >= (int)f.entries.size()) return fail(PGMI_E_ARG, "entry index out of range");
+    const StEntry& e = f.entries[i];
+    std::snprintf(name, (size_t)name_cap, "%s", e.name.c_str());
+    *dtype = e.dtype == "BF16" ? PGMI_DTYPE_BF16 : e.dtype == "F16" ? PGMI_DTYPE_F16 : e.dtype == "F32" ? PGMI_DTYPE_F32 : -1;
+    *ndim = (int)e.shape.size();
+    for (int d = 0; d < 4; ++d) shape4[d] = d < *ndim ? e.shape[d] : 0;
+    *begin = e.begin;
+    *end = e.end;
+    return 0;
+}
+
+// utils.py:19-44 (safe_open shard loop + load_state_dict(strict=False)) for one shard: tensors
+// named like slab weights are shape-checked, converted to bf16 and written into the slab; BF16
+// bytes go host -> slab directly from the mapped file, F32/F16 through the split-K scratch in
+// chunks and a device-side RNE conversion.  Synchronises the stream before unmapping.
+int pgmi_load_safetensors(pgmi_ctx* x, const char* path, int* n_loaded, int* n_skipped, void* stream) {
+    if (!x || !path) return fail(PGMI_E_ARG, "null argument");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound");
+    HIPCHK(hipSetDevice(x->device));
+    StFile f;
+    if (!st_open(path, f)) return fail(PGMI_E_ARG, f.error);
+    hipStream_t st = (hipStream_t)stream;
+    // scratch for conversions: the context's workspace if prepared, else a temporary buffer
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    uint8_t* scratch = reinterpret_cast<uint8_t*>(x->ws);
+    size_t scratch_bytes = x->ws ? x->ws_bytes : 0;
+    int loaded = 0, skipped = 0;
+    int rc = 0;
+    for (const StEntry& e : f.entries) {
+        auto it = x->index.find(e.name);
+        if (it == x->index.end()) {
+            ++skipped;
+            continue;
+        }
+        const Slot& sl = x->slots[it->second];
+        bool same = (int)e.shape.size() == sl.ndim;
+        for (int d = 0; same && d < sl.ndim; ++d) same = e.shape[d] == sl.shape[d];
+        if (!same) {
+            rc = fail(PGMI_E_ARG, "shape mismatch for " + e.name);
+            break;
+        }
+        const int eb = st_elem_bytes(e.dtype);
+        if (eb == 0) {
+            rc = fail(PGMI_E_ARG, "unsupported dtype " + e.dtype + " for " + e.name);
+            break;
+        }
+        if (e.end - e.begin != sl.numel * eb) {
+            rc = fail(PGMI_E_ARG, "byte size mismatch for " + e.name);
+            break;
+        }
+        const uint8_t* src = f.map + f.data0 + e.begin;
+        uint16_t* dst = reinterpret_cast<uint16_t*>(x->slab + sl.off);
+        if (e.dtype == "BF16") {
+            if (hipMemcpyAsync(dst, src, (size_t)sl.numel * 2, hipMemcpyHostToDevice, st) != hipSuccess) {
+                rc = fail(PGMI_E_HIP, "upload of " + e.name);
+                break;
+            }
+        } else {
+            const int dt = e.dtype == "F32" ? PGMI_DTYPE_F32 : PGMI_DTYPE_F16;
+            if (scratch_bytes < ((size_t)8 << 20)) {
+                if (!tmp) {
+                    tmp_bytes = (size_t)64 << 20;
+                    if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) {
+                        rc = fail(PGMI_E_NOMEM, "conversion scratch");
+                        break;
+                    }
+                }
+                scratch = reinterpret_cast<uint8_t*>(tmp);
+                scratch_bytes = tmp_bytes;
+            }
+            const int64_t per = (int64_t)(scratch_bytes / (size_t)eb);
+            for (int64_t i0 = 0; i0 < sl.numel && rc == 0; i0 += per) {
+                const int64_t n = std::min<int64_t>(per, sl.numel - i0);
+                if (hipMemcpyAsync(scratch, src + i0 * eb, (size_t)n * eb, hipMemcpyHostToDevice, st) != hipSuccess) {
+                    rc = fail(PGMI_E_HIP, "upload of " + e.name);
+                    break;
+                }
+                hipLaunchKernelGGL(k_convert, dim3(1024), dim3(256), 0, st, scratch, dt, (long)n, dst + i0);
+            }
+            if (rc) break;
+        }
+        ++loaded;
+    }
+    const hipError_t se = hipStreamSynchronize(st);  // the mapped bytes must outlive the copies
+    if (tmp) (void)hipFree(tmp);
+    if (rc) return rc;
+    if (se != hipSuccess) return fail(PGMI_E_HIP, std::string("safetensors upload: ") + hipGetErrorString(se));
+    x->prepared = false;  // derived tensors (padded patch matrix, ...) are rebuilt by pgmi_prepare
+    if (n_loaded) *n_loaded = loaded;
+    if (n_skipped) *n_skipped = skipped;
     return 0;
 }
 

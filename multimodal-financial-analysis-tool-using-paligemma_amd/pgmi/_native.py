@@ -49,6 +49,11 @@ SIGNATURES = {
     "pgmi_bind_weights": (i32, [vp, vp]),
     "pgmi_load_weight": (i32, [vp, ctypes.c_char_p, vp, i32, i32, vp]),
     "pgmi_fill_synthetic": (i32, [vp, ctypes.c_char_p, u64, f32, f32, vp]),
+    "pgmi_load_safetensors": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]),
+    "pgmi_safetensors_count": (i32, [ctypes.c_char_p, ctypes.POINTER(i32)]),
+    "pgmi_safetensors_entry": (i32, [ctypes.c_char_p, i32, ctypes.c_char_p, i32, ctypes.POINTER(i32),
+                                     ctypes.POINTER(i64 * 4), ctypes.POINTER(i32), ctypes.POINTER(i64),
+                                     ctypes.POINTER(i64)]),
     "pgmi_synthetic_key": (u64, [ctypes.c_char_p, u64]),
     "pgmi_set_rope_inv_freq": (i32, [vp, ctypes.POINTER(f32)]),
     "pgmi_set_rope_table": (i32, [vp, vp, vp, i32]),
@@ -115,6 +120,22 @@ def check(rc: int, what: str = ""):
 
 def ptr(t) -> "int | None":
     return None if t is None else t.data_ptr()
+
+
+def safetensors_index(path: str):
+    """[(name, dtype code, shape, begin, end)] of a safetensors file, parsed by libpgmi (no GPU)."""
+    L = lib()
+    n = ctypes.c_int()
+    check(L.pgmi_safetensors_count(path.encode(), ctypes.byref(n)), path)
+    out = []
+    for i in range(n.value):
+        name = ctypes.create_string_buffer(1024)
+        dt, nd = ctypes.c_int(), ctypes.c_int()
+        shape, b, e = (i64 * 4)(), ctypes.c_int64(), ctypes.c_int64()
+        check(L.pgmi_safetensors_entry(path.encode(), i, name, 1024, ctypes.byref(dt), ctypes.byref(shape),
+                                       ctypes.byref(nd), ctypes.byref(b), ctypes.byref(e)), path)
+        out.append((name.value.decode(), dt.value, tuple(shape[j] for j in range(nd.value)), b.value, e.value))
+    return out
 
 
 def stream_handle(device=None) -> int:

@@ -99,6 +99,29 @@ class Engine:
                 view.copy_(t.to(device=self.device, dtype=torch.bfloat16))
         self.prepared = False
 
+    def load_safetensors(self, path: str, strict: bool = True) -> int:
+        """Native safetensors loading into the slab (pgmi_load_safetensors).
+        `path` is a *.safetensors file or a directory of shards.  With strict, every slab weight
+        must come from the files.  Returns the number of tensors loaded."""
+        import glob
+        import os
+        files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
+        if not files:
+            raise FileNotFoundError(f"no *.safetensors under {path}")
+        s = N.stream_handle(self.device)
+        got = set()
+        total = 0
+        for f in files:
+            nl, ns = ctypes.c_int(), ctypes.c_int()
+            N.check(self.lib.pgmi_load_safetensors(self.ctx, f.encode(), ctypes.byref(nl), ctypes.byref(ns), s), f)
+            total += nl.value
+            got.update(e[0] for e in N.safetensors_index(f) if e[0] in self.views)
+        missing = [n for n in self.views if n not in got]
+        if strict and missing:
+            raise KeyError(f"{len(missing)} weights missing from {path}: {missing[:4]}")
+        self.prepared = False
+        return total
+
     def fill_synthetic(self, seed: int, policy):
         """Device-side deterministic init (oracle/wgen.c recipe); policy(name, shape) -> (scale, offset)."""
         s = N.stream_handle(self.device)

@@ -56,12 +56,32 @@ def load_safetensors(model, model_path: str, strict: bool = True):
     return model
 
 
-def load_hf_model(model_path, device="cuda"):
+def load_weights_native(model, model_path: str, strict: bool = True):
+    """The checkpoint read by libpgmi straight into the model's engine slab (pgmi_load_safetensors:
+    mmap, shape checks, bf16 conversion on the device); the module's bf16 parameters are views of
+    that slab, so they see the loaded values."""
+    eng = model._pgmi_engine()
+    eng.load_safetensors(model_path, strict=strict)
+    return model
+
+
+def load_hf_model(model_path, device="cuda", native: bool = True):
     from transformers import AutoTokenizer
     tokenizer = AutoTokenizer.from_pretrained(model_path, padding_side="right")
+    model = load_model(model_path, device=device, native=native)
+    return model, tokenizer
+
+
+def load_model(model_path, device="cuda", native: bool = True):
+    """config.json + *.safetensors -> PaliGemmaForConditionalGeneration (utils.py:6-46 without the
+    tokenizer).  native: libpgmi's reader fills the engine slab; else safe_open per tensor."""
     with open(f"{model_path}/config.json", "r") as f:
         config = PaliGemmaConfig(**json.load(f))
     model = build_model(config, device=device)
-    load_safetensors(model, model_path)
-    model.tie_weights()
-    return model, tokenizer
+    if native and torch.device(device).type == "cuda":
+        model.tie_weights()  # the engine binds the tied tree (lm_head = embed_tokens, utils.py:44)
+        load_weights_native(model, model_path)
+    else:
+        load_safetensors(model, model_path)
+        model.tie_weights()
+    return model

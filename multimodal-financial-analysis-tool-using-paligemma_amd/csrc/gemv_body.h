@@ -105,13 +105,46 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, DEPTH - 1>;
-    if (ub < bend) issue(S0{}, ub);
-    if constexpr (DEPTH == 2) {
-        if (ub + stride < bend) issue(S1{}, ub + stride);
-    }
-    if constexpr (F) dep_wait(dep);  // inputs of this phase are out (weights already in flight)
-
+    // register-held activation (XREG) and its RMSNorm weights: loaded unconditionally (row
+    // clamped) so no branch splits the loads; outside the fused step they go out BEFORE the
+    // weight stream, so the norm is computed while the weights are in flight (vmcnt is in
+    // order: a load issued after the weights could only be consumed after all of them landed)
     uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
+    uint4 nw[XREG ? KCW : 1];
+    auto load_x = [&]() {
+        if constexpr (XREG && MODE != GV_ORES) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const int bq = b < a.nb ? b : a.nb - 1;
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<F>(a.x + (long)bq * K + kofs + 512 * c);
+            }
+            if (a.norm_w) {
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) nw[c] = ldg16(a.norm_w + kofs + 512 * c);
+            }
+        }
+    };
+    // the latency-bound qkv projection fetches its activation first, so the RMSNorm overlaps
+    // the weight flight (measured: the streaming modes lose a little by it -- same-box A/B,
+    // tools/probes/decode_kernels.py -- and keep the weights-first order)
+    constexpr bool XFIRST = !F && MODE == GV_QKV;
+    if constexpr (XFIRST) {
+        load_x();
+        // unconditional (issue clamps the unit): a branch around the stream would make the
+        // compiler's in-order vmcnt model drain it before the activation can be used
+        issue(S0{}, ub);
+        if constexpr (DEPTH == 2) issue(S1{}, ub + stride);
+        asm volatile("" ::: "memory");  // keep the weight stream ahead of the norm (no sinking past it)
+    } else {
+        if (ub < bend) issue(S0{}, ub);
+        if constexpr (DEPTH == 2) {
+            if (ub + stride < bend) issue(S1{}, ub + stride);
+        }
+        if constexpr (F) dep_wait(dep);  // inputs of this phase are out (weights already in flight)
+        load_x();
+    }
+
     if constexpr (MODE == GV_ORES) {
         // (G <= 8 query heads of one KV head: PaliGemma's MQA, checked at pgmi_create)
         // x[b][h*256 + d] = bf16(sum_c e^(m_c - M) O_c[h][d] / sum_c e^(m_c - M) l_c), chunks in
@@ -119,7 +152,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         // every thread combines its own 8 outputs from the chunk records directly (stats and
         // partial rows in one round trip, no LDS staging of the weights, no barrier)
         const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
-        constexpr int CMAX = 8;  // chunks held in registers; longer caches take two passes
+        constexpr int CMAX = 12;  // chunks held in registers (768 keys); longer caches take two passes
         const int nitems = a.nb * K / 8;
         for (int e8 = tid; e8 < nitems; e8 += 256) {
             const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
@@ -133,14 +166,16 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             if (nch <= CMAX) {
                 f32x4 x0[CMAX], x1[CMAX];
                 float mc[CMAX], lc[CMAX];
+                // unconditional loads (chunk index clamped; records past nch are ignored below):
+                // a guarded load per chunk compiled to a branch and a wait per chunk
 #pragma unroll
-                for (int c = 0; c < CMAX; ++c)
-                    if (c < nch) {
-                        x0[c] = ldxf4<F>(pb + (long)c * kAttnPartStride);
-                        x1[c] = ldxf4<F>(pb + (long)c * kAttnPartStride + 4);
-                        mc[c] = ldxf<F>(sp + (long)c * kAttnPartStride);
-                        lc[c] = ldxf<F>(sp + (long)c * kAttnPartStride + 16);
-                    }
+                for (int c = 0; c < CMAX; ++c) {
+                    const long cs = (long)(c < nch ? c : nch - 1) * kAttnPartStride;
+                    x0[c] = ldxf4<F>(pb + cs);
+                    x1[c] = ldxf4<F>(pb + cs + 4);
+                    mc[c] = ldxf<F>(sp + cs);
+                    lc[c] = ldxf<F>(sp + cs + 16);
+                }
 #pragma unroll
                 for (int c = 0; c < CMAX; ++c)
                     if (c < nch) M = fmaxf(M, mc[c]);
@@ -174,14 +209,11 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         __syncthreads();
     } else if constexpr (XREG) {
 #pragma unroll
-        for (int b = 0; b < B; ++b)
+        for (int b = 0; b < B; ++b)  // rows past nb (clamped loads) contribute zeros
+            if (b >= a.nb)
 #pragma unroll
-            for (int c = 0; c < KCW; ++c)
-                xr[b][c] = (b < a.nb) ? ldx16<F>(a.x + (long)b * K + kofs + 512 * c) : make_uint4(0, 0, 0, 0);
+                for (int c = 0; c < KCW; ++c) xr[b][c] = make_uint4(0, 0, 0, 0);
         if (a.norm_w) {  // WK == 1: the wave holds the whole row
-            uint4 nw[KCW];  // norm weights in the same round trip as the activation
-#pragma unroll
-            for (int c = 0; c < KCW; ++c) nw[c] = ldg16(a.norm_w + kofs + 512 * c);
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 float ss = 0.f;

@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpgmi.so")
+# PGMI_LIB_PATH: an alternative build of the same library, for same-box A/B measurements only
+LIB_PATH = os.environ.get("PGMI_LIB_PATH") or os.path.join(_HERE, "libpgmi.so")
 
 PGMI_OK, PGMI_E_ARG, PGMI_E_STATE, PGMI_E_HIP, PGMI_E_NOMEM = 0, -1, -2, -3, -4
 DTYPE_BF16, DTYPE_F16, DTYPE_F32 = 0, 1, 2

@@ -103,16 +103,38 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     };
     stage_v(0);
     __syncthreads();
-    // ---- chunk-local max / exp / sum: wave w handles head rows 4w..4w+3, lane = key
+    // ---- chunk-local max / exp / sum: wave w handles head rows 4w..4w+3, lane = key.  The four
+    // rows' butterfly reductions are interleaved (four independent cross-lane chains instead of
+    // one chain four times as long)
+    {
+        float sv[4], m[4], e[4], l[4];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int h = wave * 4 + rr;
-        const float sv = S[h][lane];
-        const float m = wave_max(sv);
-        const float e = (lane < nk && h < a.G) ? expf(sv - m) : 0.f;
-        Ps[h * DPS + lane] = f2bf(e);
-        const float l = wave_sum(e);
-        if (lane == 0) { stat[0][h] = m; stat[1][h] = l; }
+        for (int rr = 0; rr < 4; ++rr) {
+            sv[rr] = S[wave * 4 + rr][lane];
+            m[rr] = sv[rr];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) m[rr] = fmaxf(m[rr], __shfl_xor(m[rr], o, 64));
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int h = wave * 4 + rr;
+            e[rr] = (lane < nk && h < a.G) ? expf(sv[rr] - m[rr]) : 0.f;
+            Ps[h * DPS + lane] = f2bf(e[rr]);
+            l[rr] = e[rr];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) l[rr] += __shfl_xor(l[rr], o, 64);
+        if (lane == 0) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                stat[0][wave * 4 + rr] = m[rr];
+                stat[1][wave * 4 + rr] = l[rr];
+            }
+        }
     }
     __syncthreads();
     // ---- O_c[h][d] = sum_t e[h][t] v[t][d] (MFMA): wave w -> d tiles 4w..4w+3; B operand by

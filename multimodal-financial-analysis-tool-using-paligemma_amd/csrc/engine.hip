@@ -111,6 +111,9 @@ struct pgmi_ctx {
     // identical pointer/shape arguments (a replay is the eager call: kernels read the same
     // addresses at run time), captured on the second such call
     bool prefill_graph = true;
+    // device step state as the last enqueued per-phase decode step leaves it (advanced in-graph)
+    bool step_known = false;
+    int step_kv = 0, step_pos = 0;
     std::map<std::vector<intptr_t>, GraphEntry> pgraphs;
 };
 
@@ -848,7 +851,9 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     int nparts = 0;
     gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax, x->pidx,
                 &nparts);
-    if (next_ids) argmax_finish(s, B, x->pmax, x->pidx, nparts, next_ids);
+    // always the last kernel: it also advances the device step state (pgmi_decode skips its
+    // host-side set when the next call continues the sequence)
+    argmax_finish(s, B, x->pmax, x->pidx, nparts, next_ids ? next_ids : x->d_next, x->step);
     return 0;
 }
 
@@ -948,10 +953,21 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
     if (!ids || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    set_step(s, x->step, kv_len, position);
+    const bool fused = fused_ok(x, B);
+    if (fused || !x->step_known || x->step_kv != kv_len || x->step_pos != position)
+        set_step(s, x->step, kv_len, position);
+    // the per-phase step advances the device state itself (k_argmax_finish); the fused one does
+    // not.  Known only once this call has enqueued its step successfully.
+    x->step_known = false;
+    auto advanced = [&]() {
+        x->step_known = !fused;
+        x->step_kv = kv_len + 1;
+        x->step_pos = position + 1;
+    };
     if (!use_graph) {
         if ((rc = decode_any(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids))) return rc;
         LAUNCHCHK();
+        advanced();
         return 0;
     }
     HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
@@ -961,6 +977,7 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
             if ((rc = decode_any(x, s, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
             LAUNCHCHK();
+            advanced();
             return 0;
         }
         HIPCHK(hipStreamSynchronize(s));
@@ -974,6 +991,7 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     }
     HIPCHK(hipGraphLaunch(ge.exec, s));
     LAUNCHCHK();
+    advanced();
     return 0;
 }
 

@@ -413,8 +413,14 @@ void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uin
 
 // ---------------------------------------------------------------- argmax (first max, torch semantics)
 __global__ void k_argmax_finish(const float* __restrict__ pmax, const int* __restrict__ pidx, int nparts,
-                                int64_t* __restrict__ out) {
+                                int64_t* __restrict__ out, StepState* adv) {
     const int b = blockIdx.x;
+    // the decode step's last kernel: every reader of the step state is done, so advance it to
+    // the next step's (kv_len + 1, position + 1); pgmi_decode then skips its host-side set
+    if (adv && b == 0 && threadIdx.x == 0) {
+        adv->kv_len += 1;
+        adv->position += 1;
+    }
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
@@ -441,8 +447,9 @@ __global__ void k_argmax_finish(const float* __restrict__ pmax, const int* __res
     if (threadIdx.x == 0) out[b] = si[0];
 }
 
-void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out) {
-    hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out);
+void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
+                   StepState* adv) {
+    hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out, adv);
 }
 
 // torch.argmax over each row of x [rows][V] (first max wins).  Stage 1: a (nb x rows) grid, each
@@ -502,7 +509,7 @@ void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, in
     const int slice = ((V + nb - 1) / nb + 3) & ~3;
     nb = (V + slice - 1) / slice;
     hipLaunchKernelGGL(k_argmax_part, dim3(nb, rows), dim3(256), 0, s, x, V, slice, pmax, pidx, out);
-    if (nb > 1) hipLaunchKernelGGL(k_argmax_finish, dim3(rows), dim3(256), 0, s, pmax, pidx, nb, out);
+    if (nb > 1) hipLaunchKernelGGL(k_argmax_finish, dim3(rows), dim3(256), 0, s, pmax, pidx, nb, out, nullptr);
 }
 
 // ---------------------------------------------------------------- synthetic weights (bench / tests)

@@ -61,7 +61,9 @@ int gemv_logits_blocks();
 int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts);
-void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out);
+// adv (may be null): the decode step state, advanced by one step (the step's last kernel)
+void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
+                   StepState* adv = nullptr);
 int argmax_scratch_parts();
 void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, int* pidx, int64_t* out);
 

@@ -149,6 +149,13 @@ int pgmi_decode_trace(pgmi_ctx* ctx, long long* host, long n_words);
 /* torch.argmax(logits, -1) over rows of a device fp32 [rows][V] matrix (inference.py:68) */
 int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* out, void* stream);
 
+/* Stop-token bookkeeping of the batched generate loop (inference.py:51,70-71, per row): rows with
+ * finished[b] != 0 get next_ids[b] = pad_id; rows whose next_ids[b] == eos_id are marked finished
+ * (their eos is kept, as the reference appends it before breaking).  n_alive (device int32, may be
+ * NULL) receives the number of rows still running.  All pointers are device memory. */
+int pgmi_eos_update(pgmi_ctx* ctx, int64_t* next_ids, int32_t* finished, int B, int64_t eos_id, int64_t pad_id,
+                    int32_t* n_alive, void* stream);
+
 /* Launch one decode kernel of `layer` on the context's decode workspace (benchmarking the
  * dominant kernel in isolation): 1 o_proj+residual, 2 RMSNorm+gate/up+GeGLU, 3 down+residual,
  * 4 final norm + lm_head (+argmax partials; layer ignored). */

@@ -1004,6 +1004,15 @@ int pgmi_argmax(pgmi_ctx* x, const float* logits, int rows, int V, int64_t* out,
     return 0;
 }
 
+int pgmi_eos_update(pgmi_ctx* x, int64_t* next_ids, int32_t* finished, int B, int64_t eos_id, int64_t pad_id,
+                    int32_t* n_alive, void* stream) {
+    if (!x || !next_ids || !finished) return fail(PGMI_E_ARG, "null argument");
+    if (B <= 0) return fail(PGMI_E_ARG, "eos_update: empty batch");
+    eos_update((hipStream_t)stream, next_ids, finished, B, eos_id, pad_id, n_alive);
+    LAUNCHCHK();
+    return 0;
+}
+
 int pgmi_decode_kernel(pgmi_ctx* x, int which, int layer, int B, void* stream) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;

@@ -452,6 +452,34 @@ void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int
     hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out, adv);
 }
 
+// ---------------------------------------------------------------- stop tokens of the batched loop
+// inference.py:70-71 per row: the reference appends the stop token, then breaks.  A row that
+// finished at an earlier step emits `pad` from then on; a row whose token is `eos` is marked
+// finished (its eos is kept).  One workgroup; n_alive = rows still running after this step.
+__global__ void k_eos_update(int64_t* __restrict__ next, int* __restrict__ finished, int B, int64_t eos,
+                             int64_t pad, int* __restrict__ n_alive) {
+    __shared__ int alive;
+    if (threadIdx.x == 0) alive = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        if (finished[b]) {
+            next[b] = pad;
+        } else if (next[b] == eos) {
+            finished[b] = 1;
+        } else {
+            ++mine;
+        }
+    }
+    if (mine) atomicAdd(&alive, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && n_alive) *n_alive = alive;
+}
+
+void eos_update(hipStream_t s, int64_t* next, int* finished, int B, int64_t eos, int64_t pad, int* n_alive) {
+    hipLaunchKernelGGL(k_eos_update, dim3(1), dim3(256), 0, s, next, finished, B, eos, pad, n_alive);
+}
+
 // torch.argmax over each row of x [rows][V] (first max wins).  Stage 1: a (nb x rows) grid, each
 // block scans a contiguous slice of a row with 16-B loads and leaves (max, first index); stage 2
 // (k_argmax_finish) reduces the nb partials of each row.  nb == 1 writes the answer directly.

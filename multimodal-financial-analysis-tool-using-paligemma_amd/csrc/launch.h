@@ -66,6 +66,7 @@ void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int
                    StepState* adv = nullptr);
 int argmax_scratch_parts();
 void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, int* pidx, int64_t* out);
+void eos_update(hipStream_t s, int64_t* next, int* finished, int B, int64_t eos, int64_t pad, int* n_alive);
 
 // ---------------------------------------------------------------- attention
 struct AttnArgs {

@@ -72,6 +72,7 @@ SIGNATURES = {
     "pgmi_decode_status": (i32, [vp, vp]),
     "pgmi_decode_trace": (i32, [vp, vp, ctypes.c_long]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),
+    "pgmi_eos_update": (i32, [vp, vp, vp, i32, i64, i64, vp, vp]),
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),
     "pgmi_tune_attention": (i32, [i32]),

@@ -316,12 +316,20 @@ class Engine:
     @torch.no_grad()
     def generate(self, input_ids: torch.Tensor, pixel_values: torch.Tensor, n_tokens: int, graph: bool = True,
                  kv: torch.Tensor = None, do_sample: bool = False, temperature: float = 0.8, top_p: float = 0.9,
-                 generator: Optional[torch.Generator] = None):
+                 generator: Optional[torch.Generator] = None, eos_token_id: Optional[int] = None,
+                 pad_token_id: Optional[int] = None, sync_every: int = 16, return_lengths: bool = False):
         """Batched generation: prefill, then n_tokens-1 decode steps
         with the next token picked on the device -- greedy argmax, or with do_sample the
         temperature + top-p draw of inference.py:64-66 -- and no host sync per token.
         Positions follow inference.py's semantics (first decode position = L + 1,
-        modeling_gemma.py:526)."""
+        modeling_gemma.py:526).
+
+        eos_token_id: the stop token of inference.py:51,70-71, applied per row on the device
+        (pgmi_eos_update): a row keeps its eos and emits pad_token_id (default: eos) after it.
+        The loop ends early once every row has stopped, checked every `sync_every` steps (one
+        host read per check instead of the reference's `.item()` per token); the result is
+        trimmed to the longest row.  return_lengths: also return int64 (B,) tokens per row up
+        to and including its eos (the length of the reference's generated_tokens)."""
         ids = input_ids.to(self.device, torch.int64)
         B, L = ids.shape
         if kv is None:
@@ -337,10 +345,35 @@ class Engine:
         step_logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
         nxt = torch.empty(B, dtype=torch.int64, device=self.device)
         cur = toks[:, 0].clone()
+        stop = eos_token_id is not None
+        if stop:
+            pad = int(eos_token_id if pad_token_id is None else pad_token_id)
+            finished = torch.zeros(B, dtype=torch.int32, device=self.device)
+            alive = torch.empty(1, dtype=torch.int32, device=self.device)
+            self._eos_update(cur, finished, int(eos_token_id), pad, alive)
+            toks[:, 0] = cur
+        n_done = n_tokens
         for t in range(1, n_tokens):
+            if stop and (t - 1) % max(1, sync_every) == 0 and int(alive.item()) == 0:
+                n_done = t
+                break
             self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=nxt, graph=graph)
             if do_sample:
                 nxt = self.sample_top_p(step_logits, top_p, temperature, u=us[t])
+            if stop:
+                self._eos_update(nxt, finished, int(eos_token_id), pad, alive)
             toks[:, t] = nxt
             cur.copy_(nxt)
-        return toks
+        if not stop:
+            return (toks, torch.full((B,), n_tokens, dtype=torch.int64, device=self.device)) if return_lengths else toks
+        toks = toks[:, :n_done]
+        hit = toks == int(eos_token_id)
+        first = torch.where(hit.any(1), hit.int().argmax(1) + 1, torch.full_like(hit[:, 0], n_done, dtype=torch.int64))
+        toks = toks[:, :int(first.max().item())].contiguous()
+        return (toks, first.to(torch.int64)) if return_lengths else toks
+
+    def _eos_update(self, next_ids: torch.Tensor, finished: torch.Tensor, eos: int, pad: int,
+                    n_alive: Optional[torch.Tensor]) -> None:
+        N.check(self.lib.pgmi_eos_update(self.ctx, next_ids.data_ptr(), finished.data_ptr(), next_ids.numel(), eos, pad,
+                                         n_alive.data_ptr() if n_alive is not None else None, self._s()),
+                "pgmi_eos_update")

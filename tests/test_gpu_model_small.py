@@ -188,3 +188,50 @@ def test_fused_step_next_ids(eng, gold):
     finally:
         eng.set_decode_fused(False)
     assert eng.decode_status() == 0
+
+
+def test_eos_stops_each_row(eng, gold):
+    """Stop token (inference.py:51,70-71) per row on the device: a row keeps its first eos and
+    emits pad after it; lengths = tokens up to and including eos; the loop ends once every row
+    has stopped and the result is trimmed to the longest row."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    pxs = torch.stack([px[0], px[0].flip(-1), px[0].flip(-2)])
+    ids = torch.from_numpy(gold["ids"]).cuda().expand(3, -1).contiguous()
+    n = 12
+    free = eng.generate(ids, pxs, n, graph=True).cpu().numpy()
+    eos = int(free[0, 3])
+    pad = -7
+    got, lens = eng.generate(ids, pxs, n, graph=True, eos_token_id=eos, pad_token_id=pad, sync_every=2,
+                             return_lengths=True)
+    got, lens = got.cpu().numpy(), lens.cpu().numpy()
+    want_len = []
+    for r in range(3):
+        hits = np.nonzero(free[r] == eos)[0]
+        want_len.append(int(hits[0]) + 1 if len(hits) else n)
+    assert list(lens) == want_len, (lens, want_len, free)
+    assert got.shape == (3, max(want_len))
+    for r in range(3):
+        k = want_len[r]
+        assert np.array_equal(got[r, :k], free[r, :k]), (r, got[r], free[r])
+        assert (got[r, k:] == pad).all(), (r, got[r])
+    # a B=1 run matches the reference loop exactly: generated tokens end at (and include) eos
+    one = eng.generate(ids[:1], pxs[:1], n, graph=True, eos_token_id=eos).cpu().numpy()
+    assert np.array_equal(one[0], free[0, :want_len[0]])
+
+
+def test_eos_update_kernel(eng):
+    """pgmi_eos_update against a host restatement on ragged rows (B = 300 > one workgroup's lanes)."""
+    g = torch.Generator().manual_seed(5)
+    B, eos, pad = 300, 1, 0
+    nxt = torch.randint(0, 4, (B,), generator=g)
+    fin = (torch.rand(B, generator=g) < 0.3).to(torch.int32)
+    want_n = torch.where(fin.bool(), torch.full_like(nxt, pad), nxt)
+    want_f = fin | (nxt == eos).to(torch.int32)
+    want_alive = int(((fin == 0) & (nxt != eos)).sum())
+    nd, fd = nxt.cuda(), fin.cuda()
+    alive = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    eng._eos_update(nd, fd, eos, pad, alive)
+    torch.cuda.synchronize()
+    assert torch.equal(nd.cpu(), want_n)
+    assert torch.equal(fd.cpu(), want_f)
+    assert int(alive.item()) == want_alive

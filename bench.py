@@ -232,15 +232,13 @@ def time_batch(cfg, dev, seed, g, B, steps, warmup):
     kv = e.new_kv(B, cap)
     pm, _, _, lg = time_prefill(e, px, ids, torch.arange(L).expand(B, L), kv, 5)
     cur = e.argmax(lg[:, 0])
-    nxt = torch.empty_like(cur)
     logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device=dev)
     step = 0
 
     def decode_step():
         nonlocal step
         step += 1
-        e.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=nxt, graph=True)
-        cur.copy_(nxt)
+        e.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=cur, graph=True)
     for _ in range(warmup):
         decode_step()
     torch.cuda.synchronize()
@@ -307,7 +305,6 @@ def main():
     # ---- decode: warmup, then exactly K timed steps (graph replay, device-side argmax)
     first = eng.argmax(lg[:, 0])
     cur = first.clone()
-    nxt = torch.empty_like(cur)
     logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device=dev)
     graph = not a.no_graph
     step = 0
@@ -315,8 +312,8 @@ def main():
     def decode_step():
         nonlocal step
         step += 1
-        eng.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=nxt, graph=graph)
-        cur.copy_(nxt)
+        # greedy feedback in place: the step reads cur's tokens first and writes the next ones last
+        eng.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=cur, graph=graph)
 
     for _ in range(a.warmup):
         decode_step()

@@ -127,7 +127,8 @@ int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, 
  *   (= attention_mask.cumsum(-1)[:, -1], modeling_gemma.py:526, i.e. kv_len + 1 after an
  *   inference.py prefill), attention over rows [0, kv_len]; logits (device fp32 [B][vocab]);
  *   next_ids (device int64 [B], may be NULL) = argmax (first max, torch.argmax semantics).
- *   use_graph != 0 replays a captured hipGraph of the whole step. */
+ *   use_graph != 0 replays a captured hipGraph of the whole step.  next_ids == ids feeds the
+ *   argmax back in place (tokens are read first, the next ones written last): no staging copy. */
 int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                 int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
 /* Batch-1 decode-step implementation: 0 (default) = one launch per phase, captured in a hipGraph;

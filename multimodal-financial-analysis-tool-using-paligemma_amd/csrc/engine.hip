@@ -57,9 +57,10 @@ struct GraphKey {
     int kv_batch, kv_max;
     float* logits;
     int64_t* next;
+    const int64_t* ids;  // the ids buffer the graph reads (the context's staging copy, or in place)
     bool operator<(const GraphKey& o) const {
-        return std::tie(fused, B, kv, kv_batch, kv_max, logits, next) <
-               std::tie(o.fused, o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next);
+        return std::tie(fused, B, kv, kv_batch, kv_max, logits, next, ids) <
+               std::tie(o.fused, o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids);
     }
 };
 
@@ -100,6 +101,7 @@ struct pgmi_ctx {
     StepState* step;
     int64_t* d_ids;
     int64_t* d_next;             // argmax target when the caller passes none
+    unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
     unsigned* step_sync = nullptr;  // fused decode step: phase counters (zeroed per launch)
     unsigned* step_err = nullptr;   // fused decode step: sticky status
     bool fused = false;             // batch-1 decode as one dataflow launch (kernels_step.hip; opt-in)
@@ -557,6 +559,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->step_sync, (size_t)decode_step_sync_words(c.t_layers)))) return rc;
         if ((rc = dalloc_t(x, &x->step_err, 4))) return rc;
+        if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
+        HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipMemset(x->step_err, 0, 4 * sizeof(unsigned)));
         HIPCHK(hipMemset(x->step_sync, 0, (size_t)decode_step_sync_words(c.t_layers) * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
@@ -849,11 +853,12 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
     }
     int nparts = 0;
-    gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax, x->pidx,
-                &nparts);
-    // always the last kernel: it also advances the device step state (pgmi_decode skips its
-    // host-side set when the next call continues the sequence)
-    argmax_finish(s, B, x->pmax, x->pidx, nparts, next_ids ? next_ids : x->d_next, x->step);
+    int64_t* nx = next_ids ? next_ids : x->d_next;
+    // the step's last work also advances the device step state (pgmi_decode skips its host-side
+    // set when the next call continues the sequence): lm_head's last workgroup, or argmax_finish
+    if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
+                     x->pidx, &nparts, x->lm_done, nx, x->step))
+        argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
     return 0;
 }
 
@@ -970,12 +975,18 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         advanced();
         return 0;
     }
-    HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-    GraphKey key{fused_ok(x, B) ? 1 : 0, B, kv, kv_batch, kv_max, logits, next_ids};
+    // in-place feedback (next_ids == ids: the step reads its tokens first and writes the next
+    // ones last) needs no staging copy; other callers' ids are staged into the context's buffer
+    const int64_t* gids = ids;
+    if (ids != next_ids) {
+        HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        gids = x->d_ids;
+    }
+    GraphKey key{fused_ok(x, B) ? 1 : 0, B, kv, kv_batch, kv_max, logits, next_ids, gids};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            if ((rc = decode_any(x, s, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
+            if ((rc = decode_any(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
             LAUNCHCHK();
             advanced();
             return 0;
@@ -983,7 +994,7 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_any(x, x->cap_stream, x->d_ids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+        rc = decode_any(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
         if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));

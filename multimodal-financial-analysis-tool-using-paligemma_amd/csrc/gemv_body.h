@@ -39,6 +39,12 @@ struct GemvArgs {
     float* logits;           // LOGITS: [nb][N]
     float* pmax;             // LOGITS: per-block partial max [nb][gridDim]
     int* pidx;
+    // LOGITS (decode): the last workgroup to finish folds every block's partial into next[b]
+    // (torch.argmax first max, inference.py:68) and advances *adv by one step -- the work of
+    // k_argmax_finish without its launch.  done: arrival counter, re-armed to 0 by that block.
+    unsigned* done;
+    int64_t* next;
+    StepState* adv;
     // QKV
     const uint16_t* cosT;
     const uint16_t* sinT;
@@ -443,8 +449,64 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                 int mi = bi[0][b];
                 for (int q = 1; q < 4; ++q)
                     if (bv[q][b] > m || (bv[q][b] == m && bi[q][b] < mi)) { m = bv[q][b]; mi = bi[q][b]; }
-                stxf<F>(a.pmax + (long)b * nblk + blk, m);
-                stxi<F>(a.pidx + (long)b * nblk + blk, mi);
+                if (a.done) {  // write-through: the folding block may sit on another XCD
+                    stf_coh(a.pmax + (long)b * nblk + blk, m);
+                    sti_coh(a.pidx + (long)b * nblk + blk, mi);
+                } else {
+                    stxf<F>(a.pmax + (long)b * nblk + blk, m);
+                    stxi<F>(a.pidx + (long)b * nblk + blk, mi);
+                }
+            }
+        }
+        if (a.done) {
+            // coh.h protocol: the storing lane drains its stores, then counts; the block whose
+            // add came last reads every partial coherently after a barrier.  Two-level count
+            // (same-address atomics serialize): block -> shard blk % 32 (own 128-B line), the
+            // block completing a shard -> top word done[0]
+            constexpr int NSH = 32, STR = 32;
+            __shared__ int last;
+            if (tid == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int sh = blk % NSH;
+                const unsigned shard_n = (unsigned)((nblk - sh + NSH - 1) / NSH);
+                const unsigned n_sh = (unsigned)(nblk < NSH ? nblk : NSH);
+                last = 0;
+                if (__hip_atomic_fetch_add(a.done + (1 + sh) * STR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+                    shard_n)
+                    last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == n_sh;
+            }
+            __syncthreads();
+            if (last) {
+                for (int b = 0; b < a.nb && b < B; ++b) {
+                    float m = -INFINITY;
+                    int mi = 0x7fffffff;
+                    for (int i = tid; i < nblk; i += blockDim.x) {
+                        const float v = ldf_coh(a.pmax + (long)b * nblk + i);
+                        const int ix = ldi_coh(a.pidx + (long)b * nblk + i);
+                        if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
+                    }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const float v = __shfl_xor(m, o);
+                        const int ix = __shfl_xor(mi, o);
+                        if (v > m || (v == m && ix < mi)) { m = v; mi = ix; }
+                    }
+                    __syncthreads();  // bv/bi reuse across rows
+                    if (lane == 0) { bv[wave][0] = m; bi[wave][0] = mi; }
+                    __syncthreads();
+                    if (tid == 0) {
+                        for (int q = 1; q < 4; ++q)
+                            if (bv[q][0] > m || (bv[q][0] == m && bi[q][0] < mi)) { m = bv[q][0]; mi = bi[q][0]; }
+                        a.next[b] = mi;
+                    }
+                }
+                if (tid == 0) {
+                    if (a.adv) {
+                        a.adv->kv_len += 1;
+                        a.adv->position += 1;
+                    }
+                }
+                if (tid <= NSH) __hip_atomic_store(a.done + tid * STR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

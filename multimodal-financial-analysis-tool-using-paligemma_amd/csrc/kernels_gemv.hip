@@ -137,8 +137,9 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
 
 int gemv_logits_blocks() { return 2048; }
 
-void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
-                 int V, float* logits, float* pmax, int* pidx, int* nparts) {
+bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
+                 int V, float* logits, float* pmax, int* pidx, int* nparts, unsigned* done, int64_t* next,
+                 StepState* adv) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
@@ -147,7 +148,13 @@ void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
     int blocks;
     if (B >= gemv_mf_min_batch()) {
         *nparts = gemv_mf_logits(s, a, mb);
-        return;
+        return false;
+    }
+    const bool fold = done && next && tune_variant("PGMI_LM_FOLD", 1) != 0;
+    if (fold) {
+        a.done = done;
+        a.next = next;
+        a.adv = adv;
     }
 #define LG_(b_, rpw)                                                    \
     do {                                                                \
@@ -170,6 +177,7 @@ void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
     else if (B <= 4) LG_(4, 2);
     else LG_(8, 2);
     *nparts = blocks;
+    return fold;
 #undef LG_
 #undef L_
 }

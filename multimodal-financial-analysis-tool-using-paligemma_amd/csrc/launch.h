@@ -59,8 +59,11 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
                 const uint16_t* Wgu, int I, uint16_t* act);
 int gemv_logits_blocks();
 int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
-void gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
-                 const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts);
+// done/next/adv (decode, may be null): fold the argmax into the launch's last workgroup and
+// advance the step state there; returns true when it did (no argmax_finish needed)
+bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
+                 const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts,
+                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr);
 // adv (may be null): the decode step state, advanced by one step (the step's last kernel)
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
                    StepState* adv = nullptr);

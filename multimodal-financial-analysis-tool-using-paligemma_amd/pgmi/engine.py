@@ -357,13 +357,14 @@ class Engine:
             if stop and (t - 1) % max(1, sync_every) == 0 and int(alive.item()) == 0:
                 n_done = t
                 break
-            self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=nxt, graph=graph)
             if do_sample:
-                nxt = self.sample_top_p(step_logits, top_p, temperature, u=us[t])
+                self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=nxt, graph=graph)
+                cur.copy_(self.sample_top_p(step_logits, top_p, temperature, u=us[t]))
+            else:  # greedy: the argmax is fed back in place (pgmi_decode with next_ids == ids)
+                self.decode(cur, kv, L + t - 1, L + t, logits=step_logits, next_ids=cur, graph=graph)
             if stop:
-                self._eos_update(nxt, finished, int(eos_token_id), pad, alive)
-            toks[:, t] = nxt
-            cur.copy_(nxt)
+                self._eos_update(cur, finished, int(eos_token_id), pad, alive)
+            toks[:, t] = cur
         if not stop:
             return (toks, torch.full((B,), n_tokens, dtype=torch.int64, device=self.device)) if return_lengths else toks
         toks = toks[:, :n_done]

@@ -235,3 +235,35 @@ def test_eos_update_kernel(eng):
     assert torch.equal(nd.cpu(), want_n)
     assert torch.equal(fd.cpu(), want_f)
     assert int(alive.item()) == want_alive
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_inplace_feedback_matches_staged(eng, gold, B):
+    """pgmi_decode with next_ids == ids (graph reads and overwrites the caller's buffer, no
+    staging copy) produces the same tokens and logits as the staged form."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    pxs = torch.stack([px[0], px[0].flip(-1), px[0].flip(-2), px[0].flip(-1).flip(-2)])[:B].contiguous()
+    ids = torch.from_numpy(gold["ids"]).cuda().expand(B, -1).contiguous()
+    L = ids.shape[1]
+    feats = eng.project(eng.vision(pxs))
+    runs = []
+    for inplace in (False, True):
+        kv = eng.new_kv(B, 1024)
+        lg = eng.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=1)
+        cur = eng.argmax(lg[:, 0])
+        nxt = torch.empty_like(cur)
+        logits = torch.empty((B, eng.cfgd["t_vocab"]), dtype=torch.float32, device="cuda")
+        seq = []
+        for t in range(1, 7):
+            if inplace:
+                eng.decode(cur, kv, L + t - 1, L + t, logits=logits, next_ids=cur, graph=True)
+            else:
+                eng.decode(cur, kv, L + t - 1, L + t, logits=logits, next_ids=nxt, graph=True)
+                cur.copy_(nxt)
+            seq.append(cur.clone())
+        torch.cuda.synchronize()
+        runs.append((torch.stack(seq, 1).cpu(), logits.cpu()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    # the argmax folded into lm_head's last workgroup == torch.argmax of the returned logits
+    assert torch.equal(runs[1][0][:, -1], runs[1][1].argmax(-1))

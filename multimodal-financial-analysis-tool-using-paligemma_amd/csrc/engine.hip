@@ -105,6 +105,14 @@ struct pgmi_ctx {
     unsigned* step_sync = nullptr;  // fused decode step: phase counters (zeroed per launch)
     unsigned* step_err = nullptr;   // fused decode step: sticky status
     bool fused = false;             // batch-1 decode as one dataflow launch (kernels_step.hip; opt-in)
+    unsigned* chain_sync = nullptr; // batch-1 attention chain counters (k_attn_chain)
+    // PGMI_CHAIN=1: batch-1 qkv -> attention -> o_proj as one launch per layer (opt-in: measured
+    // 1.285 ms/step against 1.093 ms for three launches -- same-box A/B, tools/ab3_bench.sh -- the
+    // in-launch hand-offs cost ~10 us per layer more than the two launch boundaries they replace)
+    bool chain = [] {
+        const char* v = std::getenv("PGMI_CHAIN");
+        return v && std::atoi(v) != 0;
+    }();
     long long* step_trace = nullptr;  // PGMI_STEP_TRACE=1: per-workgroup timestamps of the last step
     long step_trace_blocks = 0;
     hipStream_t cap_stream = nullptr;
@@ -559,6 +567,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->step_sync, (size_t)decode_step_sync_words(c.t_layers)))) return rc;
         if ((rc = dalloc_t(x, &x->step_err, 4))) return rc;
+        if ((rc = dalloc_t(x, &x->chain_sync, (size_t)attn_chain_sync_words(c.t_layers)))) return rc;
+        HIPCHK(hipMemset(x->chain_sync, 0, (size_t)attn_chain_sync_words(c.t_layers) * sizeof(unsigned)));
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipMemset(x->step_err, 0, 4 * sizeof(unsigned)));
@@ -824,6 +834,15 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
+static void fill_step_desc(pgmi_ctx* x, const int64_t* ids, void* kv, int kv_batch, int kv_max, float* logits,
+                           int64_t* next_ids, DecodeStepDesc& d);
+
+static bool chain_ok(const pgmi_ctx* x, int B) {
+    const pgmi_config& c = x->c;
+    return x->chain && B == 1 && gemv_logits_folds(B) && c.t_layers <= 28 && c.t_hidden == 2048 &&
+           c.t_head_dim == 256 && c.t_heads + 2 * c.t_kv_heads <= 16;
+}
+
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids) {
     const pgmi_config& c = x->c;
@@ -833,10 +852,22 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
+    // batch 1: qkv -> attention -> o_proj of a layer as one launch (k_attn_chain), its counters
+    // re-armed by the folded lm_head at the end of the step
+    const bool chain = chain_ok(x, B);
+    DecodeStepDesc cd{};
+    if (chain) fill_step_desc(x, ids, kv, kv_batch, kv_max, logits, next_ids, cd);
     embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+        if (chain) {
+            attn_chain_launch(s, cd, i, launch_keys, x->chain_sync);
+            gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
+                       c.t_intermediate, x->dACT);
+            gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
+            continue;
+        }
         gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
                  x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws);
         AttnArgs a{};
@@ -856,8 +887,10 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     int64_t* nx = next_ids ? next_ids : x->d_next;
     // the step's last work also advances the device step state (pgmi_decode skips its host-side
     // set when the next call continues the sequence): lm_head's last workgroup, or argmax_finish
+    const int cstr = attn_chain_counter_stride();
     if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
-                     x->pidx, &nparts, x->lm_done, nx, x->step))
+                     x->pidx, &nparts, x->lm_done, nx, x->step, chain ? x->chain_sync : nullptr,
+                     chain ? attn_chain_sync_words(c.t_layers) / cstr : 0, cstr))
         argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
     return 0;
 }
@@ -871,11 +904,27 @@ static bool fused_ok(const pgmi_ctx* x, int B) {
 // batch-1 step as one dataflow launch (kernels_step.hip); same arithmetic as decode_body
 static int decode_fused(pgmi_ctx* x, hipStream_t s, const int64_t* ids, void* kv, int kv_batch, int kv_max,
                         float* logits, int64_t* next_ids) {
+    DecodeStepDesc d{};
+    fill_step_desc(x, ids, kv, kv_batch, kv_max, logits, next_ids, d);
+    if (const char* tv = std::getenv("PGMI_STEP_TRACE"); tv && std::strcmp(tv, "0") != 0) {
+        const long n = decode_step_grid(d);
+        if (n > x->step_trace_blocks) {
+            int rc;
+            if ((rc = dalloc_t(x, &x->step_trace, (size_t)n * 4))) return rc;
+            x->step_trace_blocks = n;
+        }
+        d.trace = x->step_trace;
+    }
+    if (decode_step_launch(s, d)) return fail(PGMI_E_HIP, "fused decode step launch failed");
+    return 0;
+}
+
+static void fill_step_desc(pgmi_ctx* x, const int64_t* ids, void* kv, int kv_batch, int kv_max, float* logits,
+                           int64_t* next_ids, DecodeStepDesc& d) {
     const pgmi_config& c = x->c;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
-    DecodeStepDesc d{};
     d.layers = c.t_layers;
     for (int i = 0; i < c.t_layers; ++i) {
         d.ln1[i] = TL(x, i, "input_layernorm.weight");
@@ -899,17 +948,6 @@ static int decode_fused(pgmi_ctx* x, hipStream_t s, const int64_t* ids, void* kv
     d.nh = NH; d.nkv = NKV; d.H = H; d.I = c.t_intermediate; d.V = c.t_vocab;
     d.logits = logits; d.pmax = x->pmax; d.pidx = x->pidx; d.next = next_ids ? next_ids : x->d_next;
     d.sync = x->step_sync; d.err = x->step_err;
-    if (const char* tv = std::getenv("PGMI_STEP_TRACE"); tv && std::strcmp(tv, "0") != 0) {
-        const long n = decode_step_grid(d);
-        if (n > x->step_trace_blocks) {
-            int rc;
-            if ((rc = dalloc_t(x, &x->step_trace, (size_t)n * 4))) return rc;
-            x->step_trace_blocks = n;
-        }
-        d.trace = x->step_trace;
-    }
-    if (decode_step_launch(s, d)) return fail(PGMI_E_HIP, "fused decode step launch failed");
-    return 0;
 }
 
 static int decode_any(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,

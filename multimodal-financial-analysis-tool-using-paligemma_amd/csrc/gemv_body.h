@@ -45,6 +45,8 @@ struct GemvArgs {
     unsigned* done;
     int64_t* next;
     StepState* adv;
+    unsigned* rearm;         // ... and re-arms these counter words (stride rearm_stride) to 0
+    int rearm_words, rearm_stride;
     // QKV
     const uint16_t* cosT;
     const uint16_t* sinT;
@@ -507,6 +509,8 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                     }
                 }
                 if (tid <= NSH) __hip_atomic_store(a.done + tid * STR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int i = tid; i < a.rearm_words; i += blockDim.x)
+                    __hip_atomic_store(a.rearm + (long)i * a.rearm_stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

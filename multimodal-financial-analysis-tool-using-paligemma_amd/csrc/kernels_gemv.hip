@@ -137,9 +137,15 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
 
 int gemv_logits_blocks() { return 2048; }
 
+// the streaming lm_head (B < the MFMA batch) folds the argmax into its last workgroup
+bool gemv_logits_folds(int B) {
+    static const int on = tune_variant("PGMI_LM_FOLD", 1);
+    return on != 0 && B < gemv_mf_min_batch();
+}
+
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
                  int V, float* logits, float* pmax, int* pidx, int* nparts, unsigned* done, int64_t* next,
-                 StepState* adv) {
+                 StepState* adv, unsigned* rearm, int rearm_words, int rearm_stride) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
@@ -150,11 +156,14 @@ bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
         *nparts = gemv_mf_logits(s, a, mb);
         return false;
     }
-    const bool fold = done && next && tune_variant("PGMI_LM_FOLD", 1) != 0;
+    const bool fold = done && next && gemv_logits_folds(B);
     if (fold) {
         a.done = done;
         a.next = next;
         a.adv = adv;
+        a.rearm = rearm;
+        a.rearm_words = rearm ? rearm_words : 0;
+        a.rearm_stride = rearm_stride;
     }
 #define LG_(b_, rpw)                                                    \
     do {                                                                \

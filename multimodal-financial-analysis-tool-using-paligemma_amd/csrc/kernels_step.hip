@@ -219,6 +219,93 @@ __global__ void __launch_bounds__(256, 4) k_decode_step(StepArgs a) {
         __hip_atomic_store(a.sync + (long)i * kCntStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------- attention chain (batch 1)
+// One launch per layer for GemmaAttention's latency-bound chain at q_len = 1 (modeling_gemma.py:
+// 231-293): workgroup ranges [qkv:n_qkv][attn:n_attn][o:n_o] in dependency order with the
+// hand-offs of the fused step above (same bodies, same arithmetic), so the qkv -> attention ->
+// o_proj boundaries cost a counter wait instead of two kernel launches each.  The HBM-streaming
+// gate/up and down projections stay standalone launches.  Counters: 3 phases per layer, re-armed
+// by lm_head's last workgroup at the end of the step (gemv_body.h fold; every chain workgroup of
+// the step has passed its waits by then).
+struct ChainArgs {
+    StepLayerW w;
+    const StepState* st;
+    const uint16_t *cosT, *sinT;
+    int max_pos;
+    uint16_t *h, *q;
+    float* part;
+    int max_chunks;
+    long kvb;
+    int nh, nkv, H;
+    float eps, scale;
+    unsigned* sync;  // this layer's 3 phase counters
+    unsigned* err;
+    int n_qkv, n_attn, n_o, o_upb;
+};
+
+__global__ void __launch_bounds__(256, 4) k_attn_chain(ChainArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
+    auto cnt = [&](int i) { return a.sync + (long)i * kPhaseWords; };
+    Dep d;
+    d.err = a.err;
+    auto arrive_on = [&](int i, int r, int n) {
+        const int sh = r % kShards;
+        d.arrive = cnt(i);
+        d.arrive_shard = cnt(i) + (1 + sh) * kCntStride;
+        d.shard_n = (unsigned)((n - sh + kShards - 1) / kShards);
+    };
+    int r = blockIdx.x;
+    if (r < a.n_qkv) {  // inputs come from the previous launch: no wait
+        arrive_on(0, r, a.n_qkv);
+        GemvArgs g{};
+        g.x = a.h; g.norm_w = a.w.ln1; g.eps = a.eps; g.W = a.w.wqkv; g.n_units = (a.nh + 2 * a.nkv) * 128;
+        g.K = a.H; g.nb = 1; g.I = a.nh; g.out = a.q; g.cosT = a.cosT; g.sinT = a.sinT; g.max_pos = a.max_pos;
+        g.st = a.st; g.kc = a.w.kc; g.vc = a.w.vc; g.kv_b_stride = a.kvb; g.nkv = a.nkv;
+        gemv_block<1, 4, 1, GV_QKV, 1, true, true>(g, r, a.n_qkv, nullptr, d);
+        return;
+    }
+    r -= a.n_qkv;
+    const int n_chunks = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
+    if (r < a.n_attn) {
+        d.wait = cnt(0);
+        d.target = shards_of(a.n_qkv);
+        arrive_on(1, r, n_chunks);
+        const int kvd = a.nkv * 256;
+        AttnArgs at{};
+        at.q = a.q; at.q_b_stride = (long)a.nh * 256; at.q_row_stride = a.nh * 256; at.q_head_stride = 256;
+        at.k = a.w.kc; at.k_b_stride = a.kvb; at.k_row_stride = kvd; at.k_head_stride = 256;
+        at.v = a.w.vc; at.v_b_stride = a.kvb; at.v_row_stride = kvd; at.v_head_stride = 256;
+        at.Lq = 1; at.G = a.nh / a.nkv; at.n_kv = a.nkv; at.B = 1; at.scale = a.scale;
+        attn_decode_block<true>(at, a.st, a.part, a.max_chunks, r, 0, 0, lds, d);
+        return;
+    }
+    r -= a.n_attn;
+    d.wait = cnt(1);
+    d.target = shards_of(n_chunks);
+    arrive_on(2, r, a.n_o);
+    GemvArgs g{};
+    g.W = a.w.wo; g.n_units = a.H; g.K = a.nh * 256; g.nb = 1; g.out = a.h; g.part = a.part;
+    g.max_chunks = a.max_chunks; g.G = a.nh / a.nkv; g.st = a.st; g.upb = a.o_upb;
+    gemv_block<1, 4, 2, GV_ORES, 1, false, true>(g, r, a.n_o, reinterpret_cast<uint16_t*>(lds), d);
+}
+
+int attn_chain_sync_words(int layers) { return 3 * layers * kPhaseWords; }
+int attn_chain_counter_stride() { return kCntStride; }
+
+void attn_chain_launch(hipStream_t s, const DecodeStepDesc& d, int layer, int launch_keys, unsigned* sync) {
+    ChainArgs a{};
+    a.w.ln1 = d.ln1[layer]; a.w.wqkv = d.wqkv[layer]; a.w.wo = d.wo[layer]; a.w.kc = d.kc[layer]; a.w.vc = d.vc[layer];
+    a.st = d.st; a.cosT = d.cosT; a.sinT = d.sinT; a.max_pos = d.max_pos; a.h = d.h; a.q = d.q; a.part = d.part;
+    a.max_chunks = d.max_chunks; a.kvb = d.kvb; a.nh = d.nh; a.nkv = d.nkv; a.H = d.H; a.eps = d.eps;
+    a.scale = d.scale; a.sync = sync + (long)layer * 3 * kPhaseWords; a.err = d.err;
+    a.n_qkv = (d.nh + 2 * d.nkv) * 128 / 4;
+    const int nch = (launch_keys + kAttnChunk - 1) / kAttnChunk;
+    a.n_attn = nch < d.max_chunks ? nch : d.max_chunks;
+    a.o_upb = 8;  // 256 workgroups of 8 rows, as the standalone o_proj launch
+    a.n_o = (d.H + a.o_upb - 1) / a.o_upb;
+    hipLaunchKernelGGL(k_attn_chain, dim3(a.n_qkv + a.n_attn + a.n_o), dim3(256), 0, s, a);
+}
+
 // ---------------------------------------------------------------- host side
 int decode_step_sync_words(int layers) { return (2 + 5 * layers) * kPhaseWords; }
 

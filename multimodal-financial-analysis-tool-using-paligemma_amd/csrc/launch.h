@@ -63,7 +63,8 @@ int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 // advance the step state there; returns true when it did (no argmax_finish needed)
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts,
-                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr);
+                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr,
+                 unsigned* rearm = nullptr, int rearm_words = 0, int rearm_stride = 1);
 // adv (may be null): the decode step state, advanced by one step (the step's last kernel)
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
                    StepState* adv = nullptr);
@@ -166,5 +167,11 @@ struct DecodeStepDesc {
 int decode_step_sync_words(int layers);
 long decode_step_grid(const DecodeStepDesc& d);
 int decode_step_launch(hipStream_t s, const DecodeStepDesc& d);
+// batch-1 attention chain of one layer (qkv -> attention -> o_proj) as one launch; sync: the
+// chain counters (attn_chain_sync_words, zeroed; re-armed by the lm_head fold each step)
+int attn_chain_sync_words(int layers);
+int attn_chain_counter_stride();
+void attn_chain_launch(hipStream_t s, const DecodeStepDesc& d, int layer, int launch_keys, unsigned* sync);
+bool gemv_logits_folds(int B);
 
 }  // namespace pgmi

@@ -267,3 +267,32 @@ def test_inplace_feedback_matches_staged(eng, gold, B):
     assert torch.equal(runs[0][1], runs[1][1])
     # the argmax folded into lm_head's last workgroup == torch.argmax of the returned logits
     assert torch.equal(runs[1][0][:, -1], runs[1][1].argmax(-1))
+
+
+def test_attention_chain_matches_launches(eng, gold, monkeypatch):
+    """PGMI_CHAIN=1 (opt-in): qkv -> attention -> o_proj as one launch per layer with in-launch
+    hand-offs; bit-identical logits and tokens to the three-launch step over 8 graph steps."""
+    from pgmi import Engine
+    monkeypatch.setenv("PGMI_CHAIN", "1")
+    e2 = Engine(W.small_config(), max_batch=8, max_seq=640, max_kv=1024)
+    e2.fill_synthetic(SEED, W.init_policy)
+    e2.prepare()
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    L = ids.shape[1]
+    out = []
+    for e in (eng, e2):
+        kv = e.new_kv(1, 1024)
+        feats = e.project(e.vision(px))
+        lg = e.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)
+        cur = e.argmax(lg[:, 0])
+        logits = torch.empty((1, e.cfgd["t_vocab"]), dtype=torch.float32, device="cuda")
+        seq = []
+        for t in range(1, 9):
+            e.decode(cur, kv, L + t - 1, L + t, logits=logits, next_ids=cur, graph=True)
+            seq.append(int(cur.item()))
+        out.append((seq, logits.cpu(), kv[:, :, 0, :L + 9].cpu()))
+    assert e2.decode_status() == 0
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])

@@ -291,7 +291,7 @@ def test_attention_chain_matches_launches(eng, gold, monkeypatch):
         for t in range(1, 9):
             e.decode(cur, kv, L + t - 1, L + t, logits=logits, next_ids=cur, graph=True)
             seq.append(int(cur.item()))
-        out.append((seq, logits.cpu(), kv[:, :, 0, :L + 9].cpu()))
+        out.append((seq, logits.cpu(), kv[:, :, 0, :L + 8].cpu()))  # rows written: prompt + 8 steps
     assert e2.decode_status() == 0
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1])

@@ -437,7 +437,8 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
     const int KS = gridDim.y, ks = blockIdx.y;
     const int k0 = ks * KSL;
     const int n_groups = (a.n_units + 15) / 16;
-    const int gstride = gridDim.x * 4;
+    const int wpb = blockDim.x >> 6;  // streaming waves per workgroup (4; 1 for short row counts)
+    const int gstride = gridDim.x * wpb;
     uint16_t* xs = reinterpret_cast<uint16_t*>(mls);
     uint8_t* ring = mls + (((size_t)a.nb * ld * 2 + 127) & ~(size_t)127) + (size_t)wave * D * SLOT;
 
@@ -465,7 +466,7 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
                                              (__attribute__((address_space(3))) void*)(ring + slot * SLOT + q * 1024), 16, 0, 0);
         }
     };
-    int grp = blockIdx.x * 4 + wave;
+    int grp = blockIdx.x * wpb + wave;
     // the ring's first D blocks go out before the activation staging: the two round trips
     // overlap (the staging's own waits drain the ring too, so the main loop starts with every
     // counted LDS-DMA retired)
@@ -476,7 +477,7 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
     if (a.norm_w) {
         mf_stage_rows(a, K, xs, ld, red, k0, KSL);
     } else {
-        for (int c = tid * 8; c < KSL; c += 256 * 8) {
+        for (int c = tid * 8; c < KSL; c += blockDim.x * 8) {
             uint4 v[MF_MAXB];
 #pragma unroll
             for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): one round trip
@@ -688,16 +689,18 @@ static void launch_ms(hipStream_t s, const GemvArgs& a, int blocks, int KS, floa
     hipLaunchKernelGGL((k_gemv_ms<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(256), lds, s, a, ws);
 }
 
+// waves: streaming waves per workgroup (4, or fewer to spread a short row count over more CUs;
+// GV_LOGITS keeps 4: its block reduction is laid out for 4 waves)
 template <int MODE, int NR, int KSL, int D>
-static void launch_ml(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
-    const size_t lds = (((size_t)a.nb * (KSL + 8) * 2 + 127) & ~(size_t)127) + (size_t)4 * D * NR * 16 * 256;
+static void launch_ml(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws, int waves = 4) {
+    const size_t lds = (((size_t)a.nb * (KSL + 8) * 2 + 127) & ~(size_t)127) + (size_t)waves * D * NR * 16 * 256;
     static size_t attr = 0;
     if (lds > attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_ml<MODE, NR, KSL, D>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_gemv_ml<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(256), lds, s, a, ws);
+    hipLaunchKernelGGL((k_gemv_ml<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(64 * waves), lds, s, a, ws);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -738,8 +741,15 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     GemvArgs r = a;
     r.x = o;
     r.norm_w = nullptr;
-    if (env_int("PGMI_MF_ML", 1)) launch_ml<GV_RES, 1, 2048, 6>(s, r, ms_blocks(a.n_units, 256), 1, nullptr);
-    else launch_ms<GV_RES, 1, 2048, 4>(s, r, ms_blocks(a.n_units, 1024), 1, nullptr);
+    if (env_int("PGMI_MF_ML", 1)) {
+        // 2048 rows = 128 groups of 16: 4-wave workgroups would occupy only 32 CUs
+        static const int w = env_int("PGMI_MF_O_WAVES", 2);  // measured: 4 -> 1.828, 1 -> 1.812, 2 -> 1.807 ms per B = 8 step
+        const int waves = (w == 1 || w == 2) ? w : 4;
+        const int g = groups_of(a.n_units);
+        launch_ml<GV_RES, 1, 2048, 6>(s, r, (g + waves - 1) / waves, 1, nullptr, waves);
+    } else {
+        launch_ms<GV_RES, 1, 2048, 4>(s, r, ms_blocks(a.n_units, 1024), 1, nullptr);
+    }
 }
 
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2048

@@ -106,6 +106,15 @@ struct pgmi_ctx {
     unsigned* step_err = nullptr;   // fused decode step: sticky status
     bool fused = false;             // batch-1 decode as one dataflow launch (kernels_step.hip; opt-in)
     unsigned* chain_sync = nullptr; // batch-1 attention chain counters (k_attn_chain)
+    // lock-step batches of at least this many rows run the decode MLP on the prefill GEMMs
+    // (PGMI_DEC_MLP_GEMM, opt-in; 0 = never).  Measured at B = 8 (tools/b8_mlp.sh, same box):
+    // 1.92 ms per step against 1.82 ms on the MFMA GEMVs -- the separate RMSNorm and split-K
+    // epilogue launches outweigh the faster gate|up tile
+    int mlp_gemm_min = [] {
+        const char* v = std::getenv("PGMI_DEC_MLP_GEMM");
+        const int n = v ? std::atoi(v) : 0;
+        return n > 0 ? n : 1 << 30;
+    }();
     // PGMI_CHAIN=1: batch-1 qkv -> attention -> o_proj as one launch per layer (opt-in: measured
     // 1.285 ms/step against 1.093 ms for three launches -- same-box A/B, tools/ab3_bench.sh -- the
     // in-launch hand-offs cost ~10 us per layer more than the two launch boundaries they replace)
@@ -879,6 +888,20 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
                     B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+        if (B >= x->mlp_gemm_min) {
+            // lock-step batches: the MLP as the prefill's MFMA GEMMs with B rows (RMSNorm into dAO,
+            // free after o_proj; GeGLU in the gate|up epilogue; down split-K + residual)
+            rmsnorm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, x->dAO, B, H);
+            EpiArgs g{};
+            g.out = x->dACT; g.ldo = c.t_intermediate;
+            gemm(s, x->dAO, H, TL(x, i, "mlp.gate_proj.weight"), H, B, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
+                 x->ws_bytes, c.t_intermediate);
+            EpiArgs d{};
+            d.res = x->dH; d.ldr = H; d.out = x->dH; d.ldo = H;
+            gemm(s, x->dACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, B, H,
+                 c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes);
+            continue;
+        }
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);

@@ -486,6 +486,12 @@ static Plan choose(int M, int N, int K, bool dual) {
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
+    // lock-step decode batches as GEMMs (M <= 16 rows, PGMI_DEC_MLP_GEMM; tools/gemm_sweep.py b8_*
+    // in isolation: gate|up 64x128 tiles 24.2 us, down 64x64 split 8 18.1 us)
+    if (M <= 16) {
+        if (dual) return mk(P64x128, 1);
+        if (K >= 8192) return mk(P64x64, 8);
+    }
     // other shapes (batched prefill: M = B x 256 / 288 rows; other image sizes)
     if (dual) return mk(M <= 256 ? Q256w : M <= 288 ? Q288w : Q352w, 1);
     if (K >= 8192) return mk(M <= 288 ? P288n : P288w, M <= 288 ? 8 : 4);

@@ -21,6 +21,9 @@ SHAPES = {  # name: (M, N, K, epi)
     "v_proj": (256, 2048, 1152, 1),
     "t448_qkv": (1056, 2560, 2048, 0), "t448_o": (1056, 2048, 2048, 4), "t448_gateup": (1056, 16384, 2048, 7),
     "t448_down": (1056, 2048, 16384, 4), "v448_fc1": (1024, 4304, 1152, 2), "v448_qkv": (1024, 3456, 1152, 1),
+    # batched decode (configs[3]: 8 lock-step sequences) as GEMMs with 8 rows
+    "b8_gateup": (8, 16384, 2048, 7), "b8_down": (8, 2048, 16384, 4), "b8_o": (8, 2048, 2048, 4),
+    "b8_qkv": (8, 2560, 2048, 0),
 }
 
 

@@ -8,7 +8,14 @@ argmax), replayed as one hipGraph.  Inputs and weights are resident in HBM befor
 region; weights are deterministic synthetic values of the 3B architecture (no checkpoint is
 available offline).
 
-    python bench.py [--gpus N --steps K --warmup W]            (N > 1: torchrun, one rank/GPU)
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1 (BASELINE.json configs[3]: images sharded 8 per GPU): one process per GPU.  Launched by
+torchrun (WORLD_SIZE set) it runs as that rank; started directly with --gpus N > 1 it re-launches
+itself under torch.distributed.run with N ranks (a child process started before any GPU call) and
+exits with the child's status.  Each rank is an independent replica; the weights are generated on
+rank 0 and RCCL-broadcast through libpgmi's C ABI (pgmi_broadcast_weights); --batch defaults to 8
+images per GPU, and value = tokens of all ranks / the max-over-ranks timed region.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline      the dominant decode kernel (fused RMSNorm + gate/up GEMV + GeGLU), timed with
@@ -41,7 +48,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--batch", type=int, default=1, help="images (sequences) per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="images (sequences) per GPU (default 1 on one GPU -- configs[1]; 8 with N > 1 -- configs[3])")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--prefill-iters", type=int, default=20)
@@ -53,6 +61,9 @@ def parse():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the configs[2] (no KV cache) and configs[3] (8 images per GPU) measurements")
     ap.add_argument("--nokv-tokens", type=int, default=16)
+    ap.add_argument("--no-api", action="store_true",
+                    help="skip the drop-in module API leg (inference.py's loop through PaliGemmaForConditionalGeneration)")
+    ap.add_argument("--api-tokens", type=int, default=32)
     return ap.parse_args()
 
 
@@ -84,6 +95,10 @@ def cpu_baseline(cfg, seed, L, steps):
     dt = time.perf_counter() - t0
     threads = max([i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()] or [1])
     return {"value": round(steps / dt, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+            "reference_cpu": {"value": 12.2, "unit": "tokens/s", "cores": 8, "dtype": "bf16",
+                              "inference_py_semantics_tok_s": 5.2, "prefill_ms": 640,
+                              "where": "the reference's own modules timed in the survey container (8 Xeon cores, "
+                                       "torch 2.10 CPU), BASELINE.md sec.2; the reference cannot travel to the GPU box"},
             "sample": f"{steps} KV-cached greedy decode steps of oracle/paligemma_np.py (numpy fp32 with bf16 "
                       f"rounding points) at full PaliGemma-3B text shapes, batch 1, cache {L} tokens; "
                       f"weight generation ({gen_s:.0f}s) untimed"}
@@ -253,31 +268,147 @@ def time_batch(cfg, dev, seed, g, B, steps, warmup):
             "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps}
 
 
+def relaunch_multi(a) -> int:
+    """--gpus N > 1 without a torchrun environment: N ranks under torch.distributed.run, as a child
+    process started before anything touches the GPU (no exec from this process)."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def csrc_digest() -> str:
+    """sha1 over the HIP sources of libpgmi (ties a committed PMC traffic file to the code it measured)."""
+    import glob
+    import hashlib
+    h = hashlib.sha1()
+    for f in sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch of the dominant kernel from the FETCH_SIZE / WRITE_SIZE passes
+    (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/pmc_traffic.json).  Used only when the
+    file was produced from the same csrc sources as this build; otherwise null."""
+    tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    src = {"file": "profiles/pmc_traffic.json", "matches_build": False}
+    if not os.path.exists(tf):
+        return None, src
+    try:
+        d = json.load(open(tf))
+        src.update(round=d.get("round"), csrc_sha1=d.get("csrc_sha1"))
+        if d.get("csrc_sha1") != csrc_digest():
+            return None, src
+        src["matches_build"] = True
+        return d[kernel_key]["hbm_bytes_per_launch"], src
+    except Exception:
+        return None, src
+
+
+def time_api(cfg, dev, seed, tokens):
+    """The drop-in module path exactly as inference.py:55-78 drives it: PaliGemmaForConditionalGeneration
+    (synthetic 3B weights in its engine slab), prefill forward with the reference's (B, L, V)
+    logits -- the default lazy form, and the eager all-row form -- then `tokens` decode steps through
+    forward() with pixel_values re-passed, the attention mask grown by a float column, argmax of
+    logits[:, -1, :] and next_token.item() per token (the reference's host sync)."""
+    import torch
+    import modeling_gemma as MG
+    import utils as U
+    from pgmi.synthetic import init_policy, prompt_ids
+    pcfg = MG.PaliGemmaConfig(**{k: v for k, v in cfg.items() if k not in ("bos_token_id", "eos_token_id")})
+    m = U.build_model(pcfg, device=dev)
+    m.tie_weights()
+    eng = m._pgmi_engine()
+    eng.fill_synthetic(seed, init_policy)
+    eng.prepare()
+    n_img = (cfg["vision_config"]["image_size"] // 14) ** 2
+    ids0 = torch.from_numpy(prompt_ids(cfg["image_token_index"], n_img, cfg["text_config"]["vocab_size"])).to(dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+    px = (torch.rand((1, 3, 224, 224), generator=g, device=dev) * 2 - 1).contiguous()
+
+    def prefill(mode):
+        m.pgmi_prefill_logits = mode
+        kv = MG.KVCache()
+        out = m(input_ids=ids0, pixel_values=px, attention_mask=torch.ones_like(ids0), kv_cache=kv)
+        return out, kv
+
+    res = {}
+    with torch.no_grad():
+        for mode in ("lazy", "all"):
+            for _ in range(3):
+                prefill(mode)
+            ts = []
+            for _ in range(10):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out, kv = prefill(mode)
+                _ = torch.argmax(out["logits"][:, -1, :], dim=-1).item()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            res[f"prefill_ms_{mode}_logits"] = round(statistics.median(ts), 3)
+        m.pgmi_prefill_logits = "lazy"
+        ids, mask = ids0, torch.ones_like(ids0)
+        out, kv = prefill("lazy")
+        n = 0
+        t0 = None
+        for step in range(tokens + 4):
+            if step == 4:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            nxt = torch.argmax(out["logits"][:, -1, :], dim=-1, keepdim=True).squeeze(0)
+            _ = nxt.item()
+            ids = nxt.unsqueeze(-1)
+            mask = torch.cat([mask, torch.ones((1, 1), device=dev)], dim=-1)
+            out = m(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
+            n += step >= 4
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    res.update(decode_ms_per_token=round(dt * 1e3 / n, 4), decode_tok_s=round(n / dt, 1), tokens_timed=n,
+               semantics="inference.py:55-78 through the drop-in module: pixel_values re-passed, float mask column "
+                         "appended, argmax of logits[:, -1, :], .item() per token")
+    del m, eng
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_multi(a))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and not (a.gpus == 1 and world == 1):
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from pgmi import Engine
-    from pgmi.dist import broadcast_slab
+    from pgmi.dist import broadcast_weights
     from pgmi.synthetic import init_policy, paligemma_3b_config, prompt_ids
 
     cfg = paligemma_3b_config(a.image_size)
     n_img = (a.image_size // 14) ** 2
     L = n_img + 32
-    B = a.batch
+    B = a.batch if a.batch is not None else (8 if world > 1 else 1)
     kv_cap = ((L + a.warmup + a.steps + 8) + 63) // 64 * 64
     eng = Engine(cfg, device=dev, max_batch=B, max_seq=L + a.nokv_tokens, max_kv=kv_cap)
+    slab_bytes = eng.slab.numel()
 
-    # ---- weights: rank 0 generates, RCCL broadcast of the packed slab over xGMI
+    # ---- weights: rank 0 generates, one RCCL broadcast of the packed slab over xGMI (C ABI)
     bcast_ms = None
     if rank == 0:
         eng.fill_synthetic(a.seed, init_policy)
@@ -285,9 +416,10 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        broadcast_slab(eng.slab, src=0)
+        comm = broadcast_weights(eng, src=0)
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - t0) * 1e3
+        comm.close()
     eng.prepare()
 
     # ---- inputs (synthetic, resident in HBM): image per (rank, b), same prompt
@@ -352,13 +484,7 @@ def main():
     k_us = k0.elapsed_time(k1) * 1e3 / a.kernel_iters
     k_bytes = 2 * I * H * 2 + B * H * 2 + H * 2 + B * I * 2
     k_gbs = k_bytes / (k_us * 1e-6) / 1e9
-    traffic = None
-    tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf))["gateup"]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic("gateup") if B == 1 else (None, None)
 
     # ---- configs[2]: no KV cache (ablation semantics), top-p sampling cost, then configs[3]
     nokv = None
@@ -367,18 +493,18 @@ def main():
         ms_tok = time_no_kv(eng, px[:1], ids[:1], a.nokv_tokens)
         nokv = {"tokens": a.nokv_tokens, "ms_per_token": round(ms_tok, 3), "tok_s": round(1e3 / ms_tok, 1),
                 "semantics": "vision re-run + full forward over prompt + generated tokens per token"}
+    del eng, kv
+    torch.cuda.empty_cache()
     batch8 = None
     if world == 1 and not a.no_extra and B == 1:
-        del eng
-        torch.cuda.empty_cache()
         batch8 = time_batch(cfg, dev, a.seed, g, 8, 64, 8)
+    api = None
+    if world == 1 and not a.no_api and B == 1 and a.image_size == 224:
+        api = time_api(cfg, dev, a.seed, a.api_tokens)
 
     # ---- configs[4]: 448 px prefill (1024 image tokens, L = 1056) on a second context
     p448 = None
     if world == 1 and not a.no_448 and a.image_size == 224:
-        if batch8 is None:
-            del eng
-            torch.cuda.empty_cache()
         cfg4 = paligemma_3b_config(448)
         n4 = (448 // 14) ** 2
         L4 = n4 + 32
@@ -399,6 +525,13 @@ def main():
         cpu = cpu_baseline(OW.full_config(a.image_size), a.seed, L, a.cpu_steps)
 
     if rank == 0:
+        if world > 1 or B > 1:
+            workload = (f"configs[3]: paligemma-3b-pt-{a.image_size}, {B} synthetic images per GPU x {world} GPU(s) "
+                        f"(global batch {B * world}), lock-step greedy KV-cached decode after a {n_img}-image-token "
+                        f"+ 32-text-token prefill")
+        else:
+            workload = (f"configs[1]: paligemma-3b-pt-{a.image_size} greedy KV-cached decode, batch 1, after a "
+                        f"{n_img}-image-token + 32-text-token prefill")
         out = {
             "metric": "decode tokens/sec per GPU + prefill ms (224px img + 32-tok prompt), PaliGemma-3B",
             "value": round(tok_s, 3),
@@ -409,14 +542,14 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(tok_s / world / REF_DECODE_TOKS, 2),
-            "vs_baseline_ref": "RTX 2060 fp16 KV-cached decode, 256 tokens: 10.17 tok/s per GPU (BASELINE.md)",
+            "vs_baseline": None,
+            "vs_baseline_note": "BASELINE.md publishes no number for this hardware/dtype; its only decode figure is "
+                                "10.17 tok/s per GPU (RTX 2060, fp16, KV cache, 256 tokens)",
+            "per_gpu_tok_s": round(tok_s / world, 3),
             "dtype": "bf16",
             "data": "synthetic (deterministic random-init PaliGemma-3B weights, seeded random 224x224 images, "
                     "synthetic 32-token prompt)",
-            "config": {"workload": f"paligemma-3b-pt-{a.image_size} greedy KV-cached decode after a "
-                                   f"{n_img}-image-token + 32-text-token prefill",
-                       "batch_per_gpu": B, "global_batch": B * world, "prompt_len": L,
+            "config": {"workload": workload, "batch_per_gpu": B, "global_batch": B * world, "prompt_len": L,
                        "decode_tokens_timed": a.steps, "parallelism": f"replicas x{world} (weights RCCL-broadcast)",
                        "hipgraph": graph},
             "prefill_ms": round(prefill_ms, 3),
@@ -425,9 +558,9 @@ def main():
             "decode_step_hbm": {"algorithmic_bytes": step_bytes,
                                 "achieved_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                                 "frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "roofline": {"kernel": "k_gemv<B,4,2,GV_GEGLU,1> (RMSNorm + gate/up GEMV + GeGLU)",
+            "roofline": {"kernel": f"k_gemv<{B},...,GV_GEGLU> (RMSNorm + gate/up GEMV + GeGLU)",
                          "bound": "hbm", "achieved": round(k_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(k_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 3)},
             "preprocess_ms": pre_ms,
             "preprocess_workload": f"one decoded 480x640 RGB image -> {a.image_size}x{a.image_size} pixel_values (GPU)",
@@ -435,11 +568,14 @@ def main():
             "prefill_448": p448,
             "config3_no_kv": nokv,
             "config4_images_per_gpu": batch8,
+            "dropin_api": api,
             "sample_top_p_us": sample_us,
             "cpu_baseline": cpu,
         }
         if bcast_ms is not None:
             out["weight_broadcast_ms"] = round(bcast_ms, 2)
+            out["weight_broadcast_bytes"] = slab_bytes
+            out["weight_broadcast_GBs"] = round(slab_bytes / (bcast_ms * 1e-3) / 1e9, 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -131,21 +131,30 @@ int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, 
  *   argmax back in place (tokens are read first, the next ones written last): no staging copy. */
 int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                 int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
-/* Batch-1 decode-step implementation: 0 (default) = one launch per phase, captured in a hipGraph;
- * 1 (or env PGMI_DECODE_FUSED=1) = the whole step as one dataflow launch whose workgroup ranges
- * run the phases in dependency order (kernels_step.hip).  Same arithmetic, bit-identical
- * results; the per-phase launches are faster on MI355X today. */
-int pgmi_set_decode_fused(pgmi_ctx* ctx, int on);
 /* Prefill graphs (default on): pgmi_vision and pgmi_lm_forward replay a captured hipGraph when
  * called again with identical pointer and size arguments (the graph is captured on the second
  * such call; a replay reads the same addresses as the eager call would).  0 = always eager. */
 int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
-/* Sticky status of the fused step, cleared on read: bit 0 = a phase wait timed out (results of
- * that step are invalid). */
-int pgmi_decode_status(pgmi_ctx* ctx, unsigned* status);
-/* Diagnostics (env PGMI_STEP_TRACE=1): per-workgroup s_memrealtime stamps {entry, inputs ready,
- * outputs published, -} of the last fused step, copied to host; returns workgroups copied. */
-int pgmi_decode_trace(pgmi_ctx* ctx, long long* host, long n_words);
+/* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden
+ * rows: logits (device fp32 [rows][vocab]) = fp32(bf16(normed . E^T)) with the tied embedding E.
+ * Together with pgmi_lm_final_hidden this materialises the prefill's all-row logits on demand
+ * after a last-row-only pgmi_lm_forward (SURVEY.md sec.7 hard part 3: lazy logits). */
+int pgmi_lm_head(pgmi_ctx* ctx, const void* normed, int rows, float* logits, void* stream);
+/* Copies the final RMSNorm output (GemmaModel.norm, modeling_gemma.py:379) of the B*L rows of the
+ * last pgmi_lm_forward (bf16 [rows][hidden], row-major) into `out` (device memory). */
+int pgmi_lm_final_hidden(pgmi_ctx* ctx, void* out, int rows, void* stream);
+
+/* ---- replicas: the load-time weight broadcast over RCCL (xGMI).  The
+ * reference has no multi-GPU path (accelerate placement only, utils.py:27-38).  One process per
+ * GPU: the root calls pgmi_comm_unique_id, ships the PGMI_COMM_ID_BYTES bytes to every rank (any
+ * channel), each rank calls pgmi_comm_init, then pgmi_broadcast_weights copies the root's whole
+ * weight slab into every replica in one in-place ncclBroadcast; call pgmi_prepare afterwards.
+ * A host that already owns an ncclComm_t passes it as `comm` directly. */
+#define PGMI_COMM_ID_BYTES 128
+int pgmi_comm_unique_id(void* id_out);
+int pgmi_comm_init(int device, int nranks, int rank, const void* id, void** comm_out);
+int pgmi_comm_destroy(void* comm);
+int pgmi_broadcast_weights(pgmi_ctx* ctx, void* comm, int root, void* stream);
 
 /* torch.argmax(logits, -1) over rows of a device fp32 [rows][V] matrix (inference.py:68) */
 int pgmi_argmax(pgmi_ctx* ctx, const float* logits, int rows, int V, int64_t* out, void* stream);

@@ -1,6 +1,5 @@
 #pragma once
-// attn_decode_body.h -- flash-decoding workgroup body (standalone kernel: kernels_attn.hip;
-// fused decode step: kernels_step.hip).
+// attn_decode_body.h -- flash-decoding workgroup body (kernel k_attn_decode: kernels_attn.hip).
 //
 // Workgroup c owns keys [64c, 64c+64) of one (b, kv head) for all G query heads.  Scores are
 // rounded exactly as the reference (bf16(bf16(q.k) * scale), modeling_gemma.py:262-266); each
@@ -10,8 +9,6 @@
 // P.V runs on MFMA from bf16 e = exp(s - m_c) (the reference rounds the normalised p to bf16,
 // modeling_gemma.py:273,277; here the unnormalised chunk-local e is rounded, the fp32 sum l_c
 // normalises at the combine: same rounding granularity, documented in DESIGN.md).
-// F (fused step): the cache rows written before this launch are fetched BEFORE waiting for the
-// q/k/v phase; q and the new row (index kv_len) are read coherently after it.
 #include "coh.h"
 #include "common.h"
 #include "launch.h"
@@ -34,15 +31,13 @@ __device__ __forceinline__ short8 frag256(const uint16_t* rowp, bool valid, int 
     return __builtin_bit_cast(short8, ldx16<C>(rowp + k));
 }
 
-template <bool F>
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
-                                                  int max_chunks, int chunk, int kvh, int b, unsigned char* lds,
-                                                  const Dep& dep) {
+                                                  int max_chunks, int chunk, int kvh, int b, unsigned char* lds) {
     const int kv_len = st->kv_len;
     const int Lk = kv_len + 1;
     const int nch = (Lk + DCH - 1) / DCH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (chunk >= nch) return;  // (fused: no arrival; the consumer waits for nch chunks)
+    if (chunk >= nch) return;
     const int t0 = chunk * DCH;
     const int nk = (Lk - t0) < DCH ? (Lk - t0) : DCH;
     uint16_t* Vs = reinterpret_cast<uint16_t*>(lds);                          // [DVH][DVS]
@@ -50,14 +45,12 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     uint16_t* Ps = reinterpret_cast<uint16_t*>(lds + DVH * DVS * 2 + 16 * (DCH + 4) * 4);
     float (*stat)[16] = reinterpret_cast<float (*)[16]>(lds + DVH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2);
 
-    // rows already in the cache before this step (F: the new row kv_len comes after the wait)
-    const int n_old = F ? (kv_len - t0 < nk ? kv_len - t0 : nk) : nk;
     const uint16_t* vb = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
     uint4 vr[DCH * 32 / 256];
 #pragma unroll
     for (int i = 0; i < DCH * 32 / 256; ++i) {
         const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        vr[i] = r < n_old ? ldg16(vb + (long)(t0 + r) * a.v_row_stride + 8 * c) : make_uint4(0, 0, 0, 0);
+        vr[i] = r < nk ? ldg16(vb + (long)(t0 + r) * a.v_row_stride + 8 * c) : make_uint4(0, 0, 0, 0);
     }
     const int qi = lane & 15;
     const bool qvalid = qi < a.G;
@@ -66,22 +59,10 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
     short8 qf[8], kf[8];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<false>(krow, key < (F ? kv_len : Lk), kk, lane);
+    for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<false>(krow, key < Lk, kk, lane);
 
-    if constexpr (F) {
-        dep_wait(dep);
-        if (key == kv_len) {
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<true>(krow, true, kk, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < DCH * 32 / 256; ++i) {
-            const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-            if (t0 + r == kv_len) vr[i] = ld16_coh(vb + (long)kv_len * a.v_row_stride + 8 * c);
-        }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256<F>(qrow, qvalid, kk, lane);
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256<false>(qrow, qvalid, kk, lane);
 
     // ---- scores (MFMA): wave w -> keys t0 + 16w + (lane & 15)
     {
@@ -172,12 +153,11 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int h = (lane >> 4) * 4 + r;
-                if (h < a.G) stxf<F>(pb + h * 256 + ct * 16 + li, acc[j][r]);
+                if (h < a.G) stxf<false>(pb + h * 256 + ct * 16 + li, acc[j][r]);
             }
         }
     }
-    if (tid < 32) stxf<F>(pb + 16 * 256 + tid, stat[tid >> 4][tid & 15]);
-    if constexpr (F) dep_arrive(dep);
+    if (tid < 32) stxf<false>(pb + 16 * 256 + tid, stat[tid >> 4][tid & 15]);
 }
 
 }  // namespace pgmi

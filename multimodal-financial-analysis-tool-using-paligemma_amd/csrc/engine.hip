@@ -16,6 +16,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/pgmi.h"
 #include "common.h"
 #include "launch.h"
@@ -51,7 +53,6 @@ struct Slot {
 };
 
 struct GraphKey {
-    int fused;
     int B;
     void* kv;
     int kv_batch, kv_max;
@@ -59,8 +60,8 @@ struct GraphKey {
     int64_t* next;
     const int64_t* ids;  // the ids buffer the graph reads (the context's staging copy, or in place)
     bool operator<(const GraphKey& o) const {
-        return std::tie(fused, B, kv, kv_batch, kv_max, logits, next, ids) <
-               std::tie(o.fused, o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids);
+        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids) <
+               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids);
     }
 };
 
@@ -102,28 +103,6 @@ struct pgmi_ctx {
     int64_t* d_ids;
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
-    unsigned* step_sync = nullptr;  // fused decode step: phase counters (zeroed per launch)
-    unsigned* step_err = nullptr;   // fused decode step: sticky status
-    bool fused = false;             // batch-1 decode as one dataflow launch (kernels_step.hip; opt-in)
-    unsigned* chain_sync = nullptr; // batch-1 attention chain counters (k_attn_chain)
-    // lock-step batches of at least this many rows run the decode MLP on the prefill GEMMs
-    // (PGMI_DEC_MLP_GEMM, opt-in; 0 = never).  Measured at B = 8 (tools/b8_mlp.sh, same box):
-    // 1.92 ms per step against 1.82 ms on the MFMA GEMVs -- the separate RMSNorm and split-K
-    // epilogue launches outweigh the faster gate|up tile
-    int mlp_gemm_min = [] {
-        const char* v = std::getenv("PGMI_DEC_MLP_GEMM");
-        const int n = v ? std::atoi(v) : 0;
-        return n > 0 ? n : 1 << 30;
-    }();
-    // PGMI_CHAIN=1: batch-1 qkv -> attention -> o_proj as one launch per layer (opt-in: measured
-    // 1.285 ms/step against 1.093 ms for three launches -- same-box A/B, tools/ab3_bench.sh -- the
-    // in-launch hand-offs cost ~10 us per layer more than the two launch boundaries they replace)
-    bool chain = [] {
-        const char* v = std::getenv("PGMI_CHAIN");
-        return v && std::atoi(v) != 0;
-    }();
-    long long* step_trace = nullptr;  // PGMI_STEP_TRACE=1: per-workgroup timestamps of the last step
-    long step_trace_blocks = 0;
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
@@ -305,7 +284,6 @@ int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
     if (c.max_batch < 1 || c.max_batch > 8) return fail(PGMI_E_ARG, "max_batch must be in [1, 8]");
     if (c.v_hidden > 4096) return fail(PGMI_E_ARG, "v_hidden too large for the LayerNorm kernel");
     auto* x = new pgmi_ctx();
-    if (const char* v = std::getenv("PGMI_DECODE_FUSED")) x->fused = std::strcmp(v, "0") != 0;  // opt-in
     x->c = c;
     if (x->c.max_kv <= 0) x->c.max_kv = c.t_max_pos;
     x->device = device;
@@ -574,14 +552,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
-        if ((rc = dalloc_t(x, &x->step_sync, (size_t)decode_step_sync_words(c.t_layers)))) return rc;
-        if ((rc = dalloc_t(x, &x->step_err, 4))) return rc;
-        if ((rc = dalloc_t(x, &x->chain_sync, (size_t)attn_chain_sync_words(c.t_layers)))) return rc;
-        HIPCHK(hipMemset(x->chain_sync, 0, (size_t)attn_chain_sync_words(c.t_layers) * sizeof(unsigned)));
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
-        HIPCHK(hipMemset(x->step_err, 0, 4 * sizeof(unsigned)));
-        HIPCHK(hipMemset(x->step_sync, 0, (size_t)decode_step_sync_words(c.t_layers) * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
     }
     // derived tensors
@@ -843,15 +815,6 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
-static void fill_step_desc(pgmi_ctx* x, const int64_t* ids, void* kv, int kv_batch, int kv_max, float* logits,
-                           int64_t* next_ids, DecodeStepDesc& d);
-
-static bool chain_ok(const pgmi_ctx* x, int B) {
-    const pgmi_config& c = x->c;
-    return x->chain && B == 1 && gemv_logits_folds(B) && c.t_layers <= 28 && c.t_hidden == 2048 &&
-           c.t_head_dim == 256 && c.t_heads + 2 * c.t_kv_heads <= 16;
-}
-
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids) {
     const pgmi_config& c = x->c;
@@ -861,22 +824,10 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
-    // batch 1: qkv -> attention -> o_proj of a layer as one launch (k_attn_chain), its counters
-    // re-armed by the folded lm_head at the end of the step
-    const bool chain = chain_ok(x, B);
-    DecodeStepDesc cd{};
-    if (chain) fill_step_desc(x, ids, kv, kv_batch, kv_max, logits, next_ids, cd);
     embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-        if (chain) {
-            attn_chain_launch(s, cd, i, launch_keys, x->chain_sync);
-            gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
-                       c.t_intermediate, x->dACT);
-            gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
-            continue;
-        }
         gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
                  x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws);
         AttnArgs a{};
@@ -888,20 +839,6 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
                     B >= gemv_mf_min_batch() ? x->dAO : nullptr);
-        if (B >= x->mlp_gemm_min) {
-            // lock-step batches: the MLP as the prefill's MFMA GEMMs with B rows (RMSNorm into dAO,
-            // free after o_proj; GeGLU in the gate|up epilogue; down split-K + residual)
-            rmsnorm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, x->dAO, B, H);
-            EpiArgs g{};
-            g.out = x->dACT; g.ldo = c.t_intermediate;
-            gemm(s, x->dAO, H, TL(x, i, "mlp.gate_proj.weight"), H, B, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
-                 x->ws_bytes, c.t_intermediate);
-            EpiArgs d{};
-            d.res = x->dH; d.ldr = H; d.out = x->dH; d.ldo = H;
-            gemm(s, x->dACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, B, H,
-                 c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes);
-            continue;
-        }
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
@@ -910,102 +847,16 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     int64_t* nx = next_ids ? next_ids : x->d_next;
     // the step's last work also advances the device step state (pgmi_decode skips its host-side
     // set when the next call continues the sequence): lm_head's last workgroup, or argmax_finish
-    const int cstr = attn_chain_counter_stride();
     if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
-                     x->pidx, &nparts, x->lm_done, nx, x->step, chain ? x->chain_sync : nullptr,
-                     chain ? attn_chain_sync_words(c.t_layers) / cstr : 0, cstr))
+                     x->pidx, &nparts, x->lm_done, nx, x->step))
         argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
     return 0;
-}
-
-static bool fused_ok(const pgmi_ctx* x, int B) {
-    const pgmi_config& c = x->c;
-    return x->fused && B == 1 && c.t_layers <= 28 && c.t_intermediate == 16384 && c.t_hidden == 2048 &&
-           c.t_head_dim == 256 && c.t_heads + 2 * c.t_kv_heads <= 16;
-}
-
-// batch-1 step as one dataflow launch (kernels_step.hip); same arithmetic as decode_body
-static int decode_fused(pgmi_ctx* x, hipStream_t s, const int64_t* ids, void* kv, int kv_batch, int kv_max,
-                        float* logits, int64_t* next_ids) {
-    DecodeStepDesc d{};
-    fill_step_desc(x, ids, kv, kv_batch, kv_max, logits, next_ids, d);
-    if (const char* tv = std::getenv("PGMI_STEP_TRACE"); tv && std::strcmp(tv, "0") != 0) {
-        const long n = decode_step_grid(d);
-        if (n > x->step_trace_blocks) {
-            int rc;
-            if ((rc = dalloc_t(x, &x->step_trace, (size_t)n * 4))) return rc;
-            x->step_trace_blocks = n;
-        }
-        d.trace = x->step_trace;
-    }
-    if (decode_step_launch(s, d)) return fail(PGMI_E_HIP, "fused decode step launch failed");
-    return 0;
-}
-
-static void fill_step_desc(pgmi_ctx* x, const int64_t* ids, void* kv, int kv_batch, int kv_max, float* logits,
-                           int64_t* next_ids, DecodeStepDesc& d) {
-    const pgmi_config& c = x->c;
-    const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
-    const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
-    uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
-    d.layers = c.t_layers;
-    for (int i = 0; i < c.t_layers; ++i) {
-        d.ln1[i] = TL(x, i, "input_layernorm.weight");
-        d.wqkv[i] = TL(x, i, "self_attn.q_proj.weight");
-        d.wo[i] = TL(x, i, "self_attn.o_proj.weight");
-        d.ln2[i] = TL(x, i, "post_attention_layernorm.weight");
-        d.wgu[i] = TL(x, i, "mlp.gate_proj.weight");
-        d.wdn[i] = TL(x, i, "mlp.down_proj.weight");
-        d.kc[i] = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
-        d.vc[i] = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-    }
-    d.ids = ids;
-    d.E = W(x, "language_model.model.embed_tokens.weight");
-    d.fnorm = W(x, "language_model.model.norm.weight");
-    d.normalizer = bf16_round_host(std::sqrt((float)H));
-    d.eps = c.t_rms_eps;
-    d.scale = 1.0f / std::sqrt((float)HD);
-    d.pad_id = c.pad_token_id;
-    d.cosT = x->cosT; d.sinT = x->sinT; d.max_pos = c.t_max_pos; d.st = x->step;
-    d.h = x->dH; d.q = x->dQ; d.act = x->dACT; d.part = x->opart; d.max_chunks = x->max_chunks; d.kvb = kvb;
-    d.nh = NH; d.nkv = NKV; d.H = H; d.I = c.t_intermediate; d.V = c.t_vocab;
-    d.logits = logits; d.pmax = x->pmax; d.pidx = x->pidx; d.next = next_ids ? next_ids : x->d_next;
-    d.sync = x->step_sync; d.err = x->step_err;
-}
-
-static int decode_any(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
-                      int launch_keys, float* logits, int64_t* next_ids) {
-    if (fused_ok(x, B)) return decode_fused(x, s, ids, kv, kv_batch, kv_max, logits, next_ids);
-    return decode_body(x, s, ids, B, kv, kv_batch, kv_max, launch_keys, logits, next_ids);
 }
 
 int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
     x->prefill_graph = on != 0;
     clear_pgraphs(x);
-    return 0;
-}
-
-int pgmi_set_decode_fused(pgmi_ctx* x, int on) {
-    if (!x) return fail(PGMI_E_ARG, "null context");
-    x->fused = on != 0;
-    return 0;
-}
-
-int pgmi_decode_trace(pgmi_ctx* x, long long* host, long n_words) {
-    if (!x || !host) return fail(PGMI_E_ARG, "null argument");
-    if (!x->step_trace) return fail(PGMI_E_STATE, "no trace: set PGMI_STEP_TRACE=1 before the step");
-    const long n = std::min(n_words, x->step_trace_blocks * 4);
-    HIPCHK(hipMemcpy(host, x->step_trace, (size_t)n * sizeof(long long), hipMemcpyDeviceToHost));
-    return (int)(n / 4);
-}
-
-int pgmi_decode_status(pgmi_ctx* x, unsigned* status) {
-    if (!x || !status) return fail(PGMI_E_ARG, "null argument");
-    HIPCHK(hipMemcpy(status, x->step_err, sizeof(unsigned), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemset(x->step_err, 0, sizeof(unsigned)));
-    // a step that timed out may have left counters armed: start the next one from zero
-    if (*status) HIPCHK(hipMemset(x->step_sync, 0, (size_t)decode_step_sync_words(x->c.t_layers) * sizeof(unsigned)));
     return 0;
 }
 
@@ -1019,19 +870,17 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
     if (!ids || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    const bool fused = fused_ok(x, B);
-    if (fused || !x->step_known || x->step_kv != kv_len || x->step_pos != position)
-        set_step(s, x->step, kv_len, position);
-    // the per-phase step advances the device state itself (k_argmax_finish); the fused one does
-    // not.  Known only once this call has enqueued its step successfully.
+    if (!x->step_known || x->step_kv != kv_len || x->step_pos != position) set_step(s, x->step, kv_len, position);
+    // the step advances the device state itself (its last kernel); known only once this call has
+    // enqueued its step successfully
     x->step_known = false;
     auto advanced = [&]() {
-        x->step_known = !fused;
+        x->step_known = true;
         x->step_kv = kv_len + 1;
         x->step_pos = position + 1;
     };
     if (!use_graph) {
-        if ((rc = decode_any(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids))) return rc;
+        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids))) return rc;
         LAUNCHCHK();
         advanced();
         return 0;
@@ -1043,11 +892,11 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         gids = x->d_ids;
     }
-    GraphKey key{fused_ok(x, B) ? 1 : 0, B, kv, kv_batch, kv_max, logits, next_ids, gids};
+    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            if ((rc = decode_any(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
+            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
             LAUNCHCHK();
             advanced();
             return 0;
@@ -1055,7 +904,7 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_any(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
         if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
@@ -1064,6 +913,76 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     HIPCHK(hipGraphLaunch(ge.exec, s));
     LAUNCHCHK();
     advanced();
+    return 0;
+}
+
+int pgmi_lm_head(pgmi_ctx* x, const void* normed, int rows, float* logits, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (!normed || !logits) return fail(PGMI_E_ARG, "null argument");
+    if (rows < 1) return fail(PGMI_E_ARG, "lm_head: no rows");
+    const pgmi_config& c = x->c;
+    EpiArgs l{};
+    l.out_f32 = logits;
+    l.ldo = c.t_vocab;
+    gemm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(normed), c.t_hidden,
+         W(x, "language_model.model.embed_tokens.weight"), c.t_hidden, rows, c.t_vocab, c.t_hidden, EPI_F32, l, x->ws,
+         x->ws_bytes);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_lm_final_hidden(pgmi_ctx* x, void* out, int rows, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (!out) return fail(PGMI_E_ARG, "null argument");
+    if (rows < 1 || rows > x->c.max_batch * x->c.max_seq) return fail(PGMI_E_ARG, "rows exceed the prefill workspace");
+    HIPCHK(hipMemcpyAsync(out, x->Tn, (size_t)rows * x->c.t_hidden * 2, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------- replicas: load-time broadcast
+#define NCCLCHK(expr)                                                                      \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess) return fail(PGMI_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int pgmi_comm_unique_id(void* id_out) {
+    if (!id_out) return fail(PGMI_E_ARG, "null argument");
+    static_assert(sizeof(ncclUniqueId) == PGMI_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return 0;
+}
+
+int pgmi_comm_init(int device, int nranks, int rank, const void* id, void** comm_out) {
+    if (!id || !comm_out) return fail(PGMI_E_ARG, "null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PGMI_E_ARG, "bad rank / world size");
+    HIPCHK(hipSetDevice(device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    NCCLCHK(ncclCommInitRank(&comm, nranks, uid, rank));
+    *comm_out = comm;
+    return 0;
+}
+
+int pgmi_comm_destroy(void* comm) {
+    if (!comm) return 0;
+    NCCLCHK(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+    return 0;
+}
+
+int pgmi_broadcast_weights(pgmi_ctx* x, void* comm, int root, void* stream) {
+    if (!x || !comm) return fail(PGMI_E_ARG, "null argument");
+    if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound (pgmi_bind_weights)");
+    HIPCHK(hipSetDevice(x->device));
+    // the whole slab in one in-place collective: rank `root`'s bytes land in every replica
+    NCCLCHK(ncclBroadcast(x->slab, x->slab, (size_t)x->slab_bytes, ncclUint8, root, reinterpret_cast<ncclComm_t>(comm),
+                          (hipStream_t)stream));
+    x->prepared = false;  // derived tensors are rebuilt from the received weights by pgmi_prepare
     return 0;
 }
 

@@ -32,7 +32,6 @@ struct GemvArgs {
     int n_units;
     int K;
     int nb;                  // valid batch rows (<= template B)
-    int upb;                 // > 0: workgroup w owns units [w*upb, (w+1)*upb) (fused step); 0: interleaved
     int I;                   // GeGLU: up rows offset; QKV: number of q heads
     // outputs
     uint16_t* out;           // RES: h in/out [nb][N]; GEGLU: act [nb][I]; QKV: q [nb][nh*256]
@@ -45,8 +44,6 @@ struct GemvArgs {
     unsigned* done;
     int64_t* next;
     StepState* adv;
-    unsigned* rearm;         // ... and re-arms these counter words (stride rearm_stride) to 0
-    int rearm_words, rearm_stride;
     // QKV
     const uint16_t* cosT;
     const uint16_t* sinT;
@@ -68,9 +65,8 @@ struct GemvArgs {
 // XREG: the activation lives in registers (lane's own K chunks), the RMSNorm is computed
 // per wave (WK == 1: every wave holds the whole row), no LDS staging / barrier; used when
 // B * K/(512*WK) chunks fit in 32 VGPRs.  Otherwise the activation is staged in LDS.
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, bool F, int DEPTH = 1>
-__device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, const int nblk, uint16_t* xs,
-                                           const Dep& dep) {
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH = 1>
+__device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, const int nblk, uint16_t* xs) {
     constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
     constexpr int KCW = KCH / WK;  // chunks per wave
     constexpr int NL = RPW * NR * KCW;
@@ -81,10 +77,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave % WK, grp = wave / WK;
-    // unit range of this workgroup: interleaved over the grid, or one contiguous slice
-    const int stride = a.upb > 0 ? GPB * RPW : nblk * GPB * RPW;
-    int bb = a.upb > 0 ? blk * a.upb : blk * GPB * RPW;  // block-uniform loop base
-    const int bend = a.upb > 0 ? (bb + a.upb < a.n_units ? bb + a.upb : a.n_units) : a.n_units;
+    // unit groups of this workgroup: interleaved over the grid
+    const int stride = nblk * GPB * RPW;
+    int bb = blk * GPB * RPW;  // block-uniform loop base
+    const int bend = a.n_units;
     int ub = bb + grp * RPW;
     const int kofs = wk * KCW * 512 + 8 * lane;
 
@@ -114,7 +110,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, DEPTH - 1>;
     // register-held activation (XREG) and its RMSNorm weights: loaded unconditionally (row
-    // clamped) so no branch splits the loads; outside the fused step they go out BEFORE the
+    // clamped) so no branch splits the loads; they go out BEFORE the
     // weight stream, so the norm is computed while the weights are in flight (vmcnt is in
     // order: a load issued after the weights could only be consumed after all of them landed)
     uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
@@ -125,7 +121,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             for (int b = 0; b < B; ++b) {
                 const int bq = b < a.nb ? b : a.nb - 1;
 #pragma unroll
-                for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<F>(a.x + (long)bq * K + kofs + 512 * c);
+                for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<false>(a.x + (long)bq * K + kofs + 512 * c);
             }
             if (a.norm_w) {
 #pragma unroll
@@ -136,7 +132,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     // the latency-bound qkv projection fetches its activation first, so the RMSNorm overlaps
     // the weight flight (measured: the streaming modes lose a little by it -- same-box A/B,
     // tools/probes/decode_kernels.py -- and keep the weights-first order)
-    constexpr bool XFIRST = !F && MODE == GV_QKV;
+    constexpr bool XFIRST = MODE == GV_QKV;
     if constexpr (XFIRST) {
         load_x();
         // unconditional (issue clamps the unit): a branch around the stream would make the
@@ -149,7 +145,6 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         if constexpr (DEPTH == 2) {
             if (ub + stride < bend) issue(S1{}, ub + stride);
         }
-        if constexpr (F) dep_wait(dep);  // inputs of this phase are out (weights already in flight)
         load_x();
     }
 
@@ -179,10 +174,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
                 for (int c = 0; c < CMAX; ++c) {
                     const long cs = (long)(c < nch ? c : nch - 1) * kAttnPartStride;
-                    x0[c] = ldxf4<F>(pb + cs);
-                    x1[c] = ldxf4<F>(pb + cs + 4);
-                    mc[c] = ldxf<F>(sp + cs);
-                    lc[c] = ldxf<F>(sp + cs + 16);
+                    x0[c] = ldxf4<false>(pb + cs);
+                    x1[c] = ldxf4<false>(pb + cs + 4);
+                    mc[c] = ldxf<false>(sp + cs);
+                    lc[c] = ldxf<false>(sp + cs + 16);
                 }
 #pragma unroll
                 for (int c = 0; c < CMAX; ++c)
@@ -196,12 +191,12 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                         for (int j = 0; j < 4; ++j) { o[j] += w * x0[c][j]; o[4 + j] += w * x1[c][j]; }
                     }
             } else {
-                for (int c = 0; c < nch; ++c) M = fmaxf(M, ldxf<F>(sp + (long)c * kAttnPartStride));
+                for (int c = 0; c < nch; ++c) M = fmaxf(M, ldxf<false>(sp + (long)c * kAttnPartStride));
                 for (int c = 0; c < nch; ++c) {
-                    const float w = expf(ldxf<F>(sp + (long)c * kAttnPartStride) - M);
-                    S += w * ldxf<F>(sp + (long)c * kAttnPartStride + 16);
-                    const f32x4 x0 = ldxf4<F>(pb + (long)c * kAttnPartStride);
-                    const f32x4 x1 = ldxf4<F>(pb + (long)c * kAttnPartStride + 4);
+                    const float w = expf(ldxf<false>(sp + (long)c * kAttnPartStride) - M);
+                    S += w * ldxf<false>(sp + (long)c * kAttnPartStride + 16);
+                    const f32x4 x0 = ldxf4<false>(pb + (long)c * kAttnPartStride);
+                    const f32x4 x1 = ldxf4<false>(pb + (long)c * kAttnPartStride + 4);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
                 }
@@ -252,7 +247,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         for (int c = tid * 8; c < K; c += 256 * 8) {
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-                uint4 v = (b < a.nb) ? ldx16<F>(a.x + (long)b * K + c) : make_uint4(0, 0, 0, 0);
+                uint4 v = (b < a.nb) ? ldx16<false>(a.x + (long)b * K + c) : make_uint4(0, 0, 0, 0);
                 *reinterpret_cast<uint4*>(xs + b * K + c) = v;
                 if (a.norm_w) {
                     const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
@@ -312,7 +307,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             for (int b = 0; b < B; ++b) {
                 const int bq = b < a.nb ? b : a.nb - 1;
                 if constexpr (MODE == GV_RES || MODE == GV_ORES) {
-                    pre[i][b][0] = bf2f(ldxh<F>(a.out + (long)bq * a.n_units + u));
+                    pre[i][b][0] = bf2f(ldxh<false>(a.out + (long)bq * a.n_units + u));
                 } else if constexpr (MODE == GV_QKV) {
                     pre[i][b][0] = bf2f(a.cosT[(long)pos * 128 + (u & 127)]);
                     pre[i][b][1] = bf2f(a.sinT[(long)pos * 128 + (u & 127)]);
@@ -386,12 +381,12 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                 if (b >= a.nb) break;
                 if constexpr (MODE == GV_RES || MODE == GV_ORES) {
                     if (lane == 0) {
-                        stxh<F>(a.out + (long)b * a.n_units + u, f2bf(rbf(acc[i][0][b]) + pre[i][b][0]));
+                        stxh<false>(a.out + (long)b * a.n_units + u, f2bf(rbf(acc[i][0][b]) + pre[i][b][0]));
                     }
                 } else if constexpr (MODE == GV_GEGLU) {
                     if (lane == 0) {
                         const float g = rbf(gelu_tanh(rbf(acc[i][0][b])));
-                        stxh<F>(a.out + (long)b * a.I + u, f2bf(g * rbf(acc[i][1][b])));
+                        stxh<false>(a.out + (long)b * a.I + u, f2bf(g * rbf(acc[i][1][b])));
                     }
                 } else if constexpr (MODE == GV_LOGITS) {
                     const float v = rbf(acc[i][0][b]);
@@ -413,13 +408,13 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                             } else {
                                 dst = a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
                             }
-                            stxh<F>(dst + d, o0);
-                            stxh<F>(dst + d + 128, o1);
+                            stxh<false>(dst + d, o0);
+                            stxh<false>(dst + d + 128, o1);
                         } else {
                             uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) +
                                             (hh - nh - a.nkv) * 256;
-                            stxh<F>(dst + d, f2bf(x0));
-                            stxh<F>(dst + d + 128, f2bf(x1));
+                            stxh<false>(dst + d, f2bf(x0));
+                            stxh<false>(dst + d + 128, f2bf(x1));
                         }
                     }
                 }
@@ -455,8 +450,8 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                     stf_coh(a.pmax + (long)b * nblk + blk, m);
                     sti_coh(a.pidx + (long)b * nblk + blk, mi);
                 } else {
-                    stxf<F>(a.pmax + (long)b * nblk + blk, m);
-                    stxi<F>(a.pidx + (long)b * nblk + blk, mi);
+                    stxf<false>(a.pmax + (long)b * nblk + blk, m);
+                    stxi<false>(a.pidx + (long)b * nblk + blk, mi);
                 }
             }
         }
@@ -509,18 +504,15 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                     }
                 }
                 if (tid <= NSH) __hip_atomic_store(a.done + tid * STR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (int i = tid; i < a.rearm_words; i += blockDim.x)
-                    __hip_atomic_store(a.rearm + (long)i * a.rearm_stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
-    if constexpr (F) dep_arrive(dep);
 }
 
 template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH>
 __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [B][K]
-    gemv_block<B, KCH, RPW, MODE, WK, XREG, false, DEPTH>(a, blockIdx.x, gridDim.x, xs, Dep{});
+    gemv_block<B, KCH, RPW, MODE, WK, XREG, DEPTH>(a, blockIdx.x, gridDim.x, xs);
 }
 
 }  // namespace pgmi

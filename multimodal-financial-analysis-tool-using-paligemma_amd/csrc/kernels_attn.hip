@@ -513,7 +513,7 @@ int attention_prefill_max_keys(int head_dim) {
 __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a, const StepState* st, float* __restrict__ part,
                                                       int max_chunks) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
-    attn_decode_block<false>(a, st, part, max_chunks, blockIdx.x, blockIdx.y, blockIdx.z, lds, Dep{});
+    attn_decode_block(a, st, part, max_chunks, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks) {

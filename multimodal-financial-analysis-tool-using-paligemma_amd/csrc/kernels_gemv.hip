@@ -50,13 +50,7 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     }
     if (B <= 1) {
         const int cap = tune_variant("PGMI_QKV_CAP", 0);
-        const int upb = tune_variant("PGMI_QKV_UPB", 0);  // > 0: contiguous slices of upb units
-        if (upb > 0) {
-            a.upb = upb;
-            const int blocks = (a.n_units + upb - 1) / upb;
-            if (tune_variant("PGMI_QKV_DEPTH", 2) == 2) launch_gemv<1, 4, 1, GV_QKV, 1, 2>(s, a, blocks);
-            else launch_gemv<1, 4, 1, GV_QKV>(s, a, blocks);
-        } else if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
+        if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
         else launch_gemv<1, 4, 1, GV_QKV>(s, a, cap);
     }
     else if (B <= 2) L_(2, 4, 1, GV_QKV);
@@ -145,7 +139,7 @@ bool gemv_logits_folds(int B) {
 
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
                  int V, float* logits, float* pmax, int* pidx, int* nparts, unsigned* done, int64_t* next,
-                 StepState* adv, unsigned* rearm, int rearm_words, int rearm_stride) {
+                 StepState* adv) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
@@ -161,9 +155,6 @@ bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
         a.done = done;
         a.next = next;
         a.adv = adv;
-        a.rearm = rearm;
-        a.rearm_words = rearm ? rearm_words : 0;
-        a.rearm_stride = rearm_stride;
     }
 #define LG_(b_, rpw)                                                    \
     do {                                                                \

@@ -63,8 +63,7 @@ int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 // advance the step state there; returns true when it did (no argmax_finish needed)
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts,
-                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr,
-                 unsigned* rearm = nullptr, int rearm_words = 0, int rearm_stride = 1);
+                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr);
 // adv (may be null): the decode step state, advanced by one step (the step's last kernel)
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
                    StepState* adv = nullptr);
@@ -132,46 +131,6 @@ void sample_top_p(hipStream_t s, const float* x, int rows, int V, float temperat
                   void* scratch, int64_t* out, float* kept_mass);
 
 
-// ---- fused decode step (kernels_step.hip): batch 1, one launch per token
-struct DecodeStepDesc {
-    int layers;
-    const uint16_t* ln1[28];
-    const uint16_t* wqkv[28];
-    const uint16_t* wo[28];
-    const uint16_t* ln2[28];
-    const uint16_t* wgu[28];
-    const uint16_t* wdn[28];
-    uint16_t* kc[28];
-    uint16_t* vc[28];
-    const int64_t* ids;
-    const uint16_t* E;
-    const uint16_t* fnorm;
-    float normalizer, eps, scale;
-    long long pad_id;
-    const uint16_t *cosT, *sinT;
-    int max_pos;
-    const StepState* st;
-    uint16_t *h, *q, *act;
-    float* part;
-    int max_chunks;
-    long kvb;
-    int nh, nkv, H, I, V;
-    float* logits;
-    float* pmax;
-    int* pidx;
-    int64_t* next;
-    unsigned* sync;
-    unsigned* err;
-    long long* trace;  // nullptr, or [grid][4] per-workgroup timestamps (diagnostics)
-};
-int decode_step_sync_words(int layers);
-long decode_step_grid(const DecodeStepDesc& d);
-int decode_step_launch(hipStream_t s, const DecodeStepDesc& d);
-// batch-1 attention chain of one layer (qkv -> attention -> o_proj) as one launch; sync: the
-// chain counters (attn_chain_sync_words, zeroed; re-armed by the lm_head fold each step)
-int attn_chain_sync_words(int layers);
-int attn_chain_counter_stride();
-void attn_chain_launch(hipStream_t s, const DecodeStepDesc& d, int layer, int launch_keys, unsigned* sync);
 bool gemv_logits_folds(int B);
 
 }  // namespace pgmi

@@ -29,6 +29,7 @@ from torch.nn import CrossEntropyLoss
 
 from modeling_siglip import SiglipVisionConfig, SiglipVisionModel
 from pgmi import binding as _binding
+from pgmi.lazy_logits import LazyLogits
 
 
 class KVCache:
@@ -368,9 +369,11 @@ class PaliGemmaForConditionalGeneration(nn.Module):
     """modeling_gemma.py:440-617."""
 
     # knobs of the MI355X path (not in the reference): decode steps replay a captured hipGraph;
-    # prefill logits for every position (reference behaviour) or only the last one
+    # prefill logits: "lazy" (default: the (B, L, V) result computes its last row at once and the
+    # other rows only when something reads them -- pgmi/lazy_logits.py), "all" (every row eagerly,
+    # the reference's behaviour) or "last" (a (B, 1, V) tensor)
     pgmi_use_graph: bool = True
-    pgmi_prefill_logits: str = "all"
+    pgmi_prefill_logits: str = "lazy"
 
     def __init__(self, config: PaliGemmaConfig):
         super().__init__()
@@ -455,7 +458,10 @@ class PaliGemmaForConditionalGeneration(nn.Module):
         cache_len = kv_cache.num_items() if kv_cache is not None else 0
         src = input_ids if input_ids is not None else inputs_embeds
         B, L = src.shape[0], src.shape[1]
-        last_only = self.pgmi_prefill_logits == "last"
+        mode = self.pgmi_prefill_logits
+        if mode not in ("lazy", "all", "last"):
+            raise ValueError(f"pgmi_prefill_logits must be 'lazy', 'all' or 'last', not {mode!r}")
+        rows = 0 if mode == "all" else 1
 
         if self._merge_is_patched() or inputs_embeds is not None:
             # generic path: the (patched) merge decides embeddings / positions
@@ -469,13 +475,16 @@ class PaliGemmaForConditionalGeneration(nn.Module):
                 image_features=img, inputs_embeds=inputs_embeds.to(dev), input_ids=input_ids.to(dev),
                 attention_mask=attention_mask, kv_cache=kv_cache)
             pos = _positions_2d(position_ids, B, L)
-            logits = _run_lm(eng, kv_cache, B, L, pos, embeds=merged, logits_rows=1 if last_only else 0)
+            logits = _run_lm(eng, kv_cache, B, L, pos, embeds=merged, logits_rows=rows)
+            if mode == "lazy":
+                logits = LazyLogits(logits, eng.final_hidden(B * L), eng.lm_head, B, L)
         elif cache_len == 0 or kv_cache is None:
             # prefill (modeling_gemma.py:532-535: positions 0..L-1), merge on the device
             img = eng.project(eng.vision(pixel_values)) if pixel_values is not None else None
             pos = torch.arange(L).unsqueeze(0).expand(B, L)
-            logits = _run_lm(eng, kv_cache, B, L, pos, ids=input_ids, image_feats=img,
-                             logits_rows=1 if last_only else 0)
+            logits = _run_lm(eng, kv_cache, B, L, pos, ids=input_ids, image_feats=img, logits_rows=rows)
+            if mode == "lazy":
+                logits = LazyLogits(logits, eng.final_hidden(B * L), eng.lm_head, B, L)
         else:
             # KV-cached decode step; pixel_values of inference.py's loop would only produce image
             # features that the merge discards (the new token is not <image>), so they are skipped

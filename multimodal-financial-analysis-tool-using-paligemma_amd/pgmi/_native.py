@@ -65,13 +65,16 @@ SIGNATURES = {
     "pgmi_embed": (i32, [vp, vp, i32, vp, vp]),
     "pgmi_lm_forward": (i32, [vp, vp, vp, i32, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
     "pgmi_decode": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
-    "pgmi_set_decode_fused": (i32, [vp, i32]),
     "pgmi_set_prefill_graph": (i32, [vp, i32]),
     "pgmi_prefill_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_preprocess": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
-    "pgmi_decode_status": (i32, [vp, vp]),
-    "pgmi_decode_trace": (i32, [vp, vp, ctypes.c_long]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),
+    "pgmi_lm_head": (i32, [vp, vp, i32, vp, vp]),
+    "pgmi_lm_final_hidden": (i32, [vp, vp, i32, vp]),
+    "pgmi_comm_unique_id": (i32, [vp]),
+    "pgmi_comm_init": (i32, [i32, i32, i32, vp, ctypes.POINTER(vp)]),
+    "pgmi_comm_destroy": (i32, [vp]),
+    "pgmi_broadcast_weights": (i32, [vp, vp, i32, vp]),
     "pgmi_eos_update": (i32, [vp, vp, vp, i32, i64, i64, vp, vp]),
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),

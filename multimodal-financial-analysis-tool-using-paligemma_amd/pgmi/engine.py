@@ -258,6 +258,20 @@ class Engine:
                 "pgmi_lm_forward")
         return out
 
+    def final_hidden(self, rows: int) -> torch.Tensor:
+        """The final RMSNorm output of the last lm_forward's rows (B*L, hidden) bf16 (a copy)."""
+        out = torch.empty((rows, self.cfgd["t_hidden"]), dtype=torch.bfloat16, device=self.device)
+        N.check(self.lib.pgmi_lm_final_hidden(self.ctx, out.data_ptr(), rows, self._s()), "pgmi_lm_final_hidden")
+        return out
+
+    def lm_head(self, normed: torch.Tensor) -> torch.Tensor:
+        """lm_head + .float() (modeling_gemma.py:417-418) over final-normed rows -> (rows, V) fp32."""
+        self._ready()
+        x = normed.to(self.device, torch.bfloat16).reshape(-1, normed.shape[-1]).contiguous()
+        out = torch.empty((x.shape[0], self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        N.check(self.lib.pgmi_lm_head(self.ctx, x.data_ptr(), x.shape[0], out.data_ptr(), self._s()), "pgmi_lm_head")
+        return out
+
     def decode(self, ids: torch.Tensor, kv: torch.Tensor, kv_len: int, position: int, logits: torch.Tensor = None,
                next_ids: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
         """One KV-cached decode step for B sequences; returns logits (B, V) fp32."""
@@ -271,19 +285,9 @@ class Engine:
                 "pgmi_decode")
         return logits
 
-    def set_decode_fused(self, on: bool) -> None:
-        """Batch-1 decode as one dataflow launch per token (opt-in) or one launch per phase (default)."""
-        N.check(self.lib.pgmi_set_decode_fused(self.ctx, int(bool(on))), "pgmi_set_decode_fused")
-
     def set_prefill_graph(self, on: bool) -> None:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
-
-    def decode_status(self) -> int:
-        """Sticky status of the fused decode step (bit 0: a phase wait timed out); cleared on read."""
-        st = ctypes.c_uint(0)
-        N.check(self.lib.pgmi_decode_status(self.ctx, ctypes.addressof(st)), "pgmi_decode_status")
-        return int(st.value)
 
     def argmax(self, logits: torch.Tensor) -> torch.Tensor:
         l2 = logits.reshape(-1, logits.shape[-1]).contiguous()

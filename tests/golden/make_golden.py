@@ -322,12 +322,117 @@ def make_full(pixels, n_tokens=64):
                         **summarize_steps(last, sidx))
 
 
+def seeded_image(i):
+    """Synthetic RGB test image i (5..7 of the batch): seeded smooth gradients + noise at a
+    non-square size, written as PNG so the reference's own Image.open / BICUBIC path reads it."""
+    from PIL import Image
+    rng = np.random.default_rng(100 + i)
+    h, w = 300 + 17 * i, 260 + 29 * i
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = np.stack([(yy * (1 + c) + xx * (3 - c)) % 256 for c in range(3)], -1).astype(np.float64)
+    img = np.clip(base * 0.6 + rng.integers(0, 100, (h, w, 3)), 0, 255).astype(np.uint8)
+    path = f"/tmp/pgmi_seeded_{i}.png"
+    Image.fromarray(img).save(path)
+    return path
+
+
+def make_batch_images(n_tokens=64, n_sample=256):
+    """configs[3] parity target: eight distinct images (the 5 COCO jpgs + 3 seeded PNGs), each with
+    its own synthetic prompt, run ONE AT A TIME through inference.test_inference (the reference
+    cannot batch: processing_paligemma.py:80, modeling_gemma.py:526-528).  The build runs them as
+    one B = 8 batch and compares each row with its own image's fixture."""
+    from PIL import Image
+    cfg = W.full_config(224)
+    V = cfg["text_config"]["vocab_size"]
+    sidx = sample_idx(V)[:: max(1, N_SAMPLE_IDX // n_sample)]
+    t0 = time.time()
+    model, _ = build_model(cfg, torch.bfloat16)
+    print(f"built full bf16 model in {time.time() - t0:.1f}s")
+    paths = COCO + [seeded_image(i) for i in range(5, 8)]
+    res = {"sample_idx": sidx}
+    ids_all, u8_all, toks_all, ti_all, tv_all, mg_all, sv_all = [], [], [], [], [], [], []
+    for i, p in enumerate(paths):
+        ids = prompt_ids(cfg, seed=7 + i)
+        u8 = np.array(RP.resize(Image.open(p), (224, 224), resample=Image.Resampling.BICUBIC))
+        assert np.array_equal(pixels_from_u8(u8), reference_pixels(p, 224).astype(np.float32)), p
+        t0 = time.time()
+        toks, step_logits = run_test_inference(model, cfg, ids, p, n_tokens)
+        print(f"image {i}: {n_tokens} tokens in {time.time() - t0:.1f}s: {toks.tolist()[:16]}...")
+        s = summarize_steps(step_logits, sidx)
+        ids_all.append(ids[0]), u8_all.append(u8), toks_all.append(toks.reshape(-1))
+        ti_all.append(s["topk_idx"]), tv_all.append(s["topk_val"]), mg_all.append(s["margin"])
+        sv_all.append(s["sample_vals"])
+    res.update(ids=np.stack(ids_all), u8=np.stack(u8_all), tokens=np.stack(toks_all), topk_idx=np.stack(ti_all),
+               topk_val=np.stack(tv_all), margin=np.stack(mg_all), sample_vals=np.stack(sv_all))
+    np.savez_compressed(os.path.join(HERE, "full_batch8_bf16.npz"), **res)
+    print("full_batch8_bf16.npz written")
+
+
+def make_long(pixels, n_tokens=256):
+    """configs[1] as BASELINE.json states it: 256 greedy tokens with the KV cache (KV length up to
+    L + 256 + 1), through inference.test_inference, plus the prefill's ALL-ROW logits
+    (modeling_gemma.py:417-418: (1, L, 257216) fp32) summarised per row; then the fp32 truth
+    teacher-forced on the same token path."""
+    cfg = W.full_config(224)
+    V = cfg["text_config"]["vocab_size"]
+    sidx = sample_idx(V)
+    ids = prompt_ids(cfg)
+    model, _ = build_model(cfg, torch.bfloat16)
+    prefill = {}
+    orig_forward = model.forward
+
+    def spy(*a, **k):
+        out = orig_forward(*a, **k)
+        if not prefill:
+            lg = out["logits"][0].float().numpy()          # (L, V): every prefill row
+            ti, tv = topk(lg, 8)
+            prefill.update(rows_topk_idx=ti, rows_topk_val=tv, rows_sum=lg.astype(np.float64).sum(-1),
+                           rows_sumsq=(lg.astype(np.float64) ** 2).sum(-1), rows_sample_vals=lg[::8][:, sidx])
+        return out
+
+    model.forward = spy
+    t0 = time.time()
+    try:
+        toks, step_logits = run_test_inference(model, cfg, ids, COCO[0], n_tokens)
+    finally:
+        model.forward = orig_forward
+    print(f"full bf16 greedy {n_tokens} tokens in {time.time() - t0:.1f}s")
+    res = {"ids": ids, "tokens": toks.reshape(-1), "sample_idx": sidx, **summarize_steps(step_logits, sidx),
+           **prefill}
+    np.savez_compressed(os.path.join(HERE, "full256_bf16.npz"), **res)
+    del model
+    model, _ = build_model(cfg, torch.float32)
+    px = torch.from_numpy(pixels["px_0_224"][None])
+    kv = RG.KVCache()
+    mask = torch.ones((1, ids.shape[1]), dtype=torch.int64)
+    cur = torch.from_numpy(ids)
+    fl = []
+    with torch.no_grad():
+        for step in range(n_tokens):
+            out = model(input_ids=cur, pixel_values=px if step == 0 else None, attention_mask=mask, kv_cache=kv)
+            fl.append(out["logits"][:, -1, :].float().numpy()[:, sidx])
+            cur = torch.tensor([[int(toks.reshape(-1)[step])]])
+            mask = torch.cat([mask, torch.ones((1, 1))], dim=-1)
+    np.savez_compressed(os.path.join(HERE, "full256_fp32.npz"), sample_idx=sidx,
+                        sample_vals=np.concatenate(fl, 0))
+    print("full256_{bf16,fp32}.npz written")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
+    ap.add_argument("--only", choices=["batch8", "long"], default=None,
+                    help="generate only the round-2 fixtures (full_batch8 / full256)")
     a = ap.parse_args()
     torch.set_num_threads(8)
-    px = make_pixels()
-    make_small(px)
-    if not a.skip_full:
-        make_full(px)
+    px = make_pixels() if a.only != "batch8" else None
+    if a.only == "batch8":
+        make_batch_images()
+    elif a.only == "long":
+        make_long(px)
+    else:
+        make_small(px)
+        if not a.skip_full:
+            make_full(px)
+            make_batch_images()
+            make_long(px)

@@ -30,10 +30,11 @@ def rel(a, b):
 def G(golden_dir):
     load = lambda n: np.load(os.path.join(golden_dir, n))  # noqa: E731
     return {"bf16": load("full_bf16.npz"), "fp32": load("full_fp32.npz"), "nokv": load("full_nokv_bf16.npz"),
-            "448": load("full448_bf16.npz"), "px": load("pixels.npz")}
+            "448": load("full448_bf16.npz"), "px": load("pixels.npz"), "bf16_256": load("full256_bf16.npz"),
+            "fp32_256": load("full256_fp32.npz")}
 
 
-def _engine(image_size, max_seq=320, max_kv=512):
+def _engine(image_size, max_seq=320, max_kv=576):
     from pgmi import Engine
     e = Engine(W.full_config(image_size), max_batch=1, max_seq=max_seq, max_kv=max_kv)
     e.fill_synthetic(SEED, W.init_policy)
@@ -53,22 +54,19 @@ def _px(G, key):
     return torch.from_numpy(pixels_from_u8(G["px"][key])[None]).cuda()
 
 
-@torch.no_grad()
-def test_teacher_forced_64_steps(eng224, G):
-    e = eng224
-    gb, gf = G["bf16"], G["fp32"]
+def _teacher_forced(e, G, gb, gf, n):
     ids = torch.from_numpy(gb["ids"]).cuda()
     L = ids.shape[1]
     ref_toks = gb["tokens"].reshape(-1)
     sidx = torch.from_numpy(gb["sample_idx"]).cuda()
-    kv = e.new_kv(1, 512)
+    kv = e.new_kv(1, 576)
     feats = e.project(e.vision(_px(G, "u8_0_224")))
     lg = e.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)[:, 0]
     steps_logits = [lg]
-    for t in range(1, 64):
+    for t in range(1, n):
         cur = torch.tensor([int(ref_toks[t - 1])], device="cuda")
-        steps_logits.append(e.decode(cur, kv, L + t - 1, L + t).clone())
-    ours = torch.cat(steps_logits, 0)                       # (64, V)
+        steps_logits.append(e.decode(cur, kv, L + t - 1, L + t, graph=True).clone())
+    ours = torch.cat(steps_logits, 0)                       # (n, V)
     ours_s = ours[:, sidx].cpu().numpy()
     top_idx = torch.from_numpy(gb["topk_idx"]).cuda()
     ours_top = torch.gather(ours, 1, top_idx).cpu().numpy()
@@ -79,18 +77,32 @@ def test_teacher_forced_64_steps(eng224, G):
     decisive = gb["margin"] > 0.25
     assert np.array_equal(am[decisive], ref_toks[decisive]), (am, ref_toks)
     # error vs fp32 truth relative to the reference's own bf16 error
-    err_ours = np.mean([rel(ours_s[t], gf["sample_vals"][t]) for t in range(64)])
-    err_ref = np.mean([rel(gb["sample_vals"][t], gf["sample_vals"][t]) for t in range(64)])
+    err_ours = np.mean([rel(ours_s[t], gf["sample_vals"][t]) for t in range(n)])
+    err_ref = np.mean([rel(gb["sample_vals"][t], gf["sample_vals"][t]) for t in range(n)])
     assert err_ours <= 1.5 * err_ref, (err_ours, err_ref)
-    # closeness to the reference bf16 itself
-    assert np.mean([rel(ours_s[t], gb["sample_vals"][t]) for t in range(64)]) < 3e-2
+    # closeness to the reference bf16 itself, on average and at every step
+    per_step = [rel(ours_s[t], gb["sample_vals"][t]) for t in range(n)]
+    assert np.mean(per_step) < 3e-2 and max(per_step) < 6e-2, (np.mean(per_step), max(per_step))
 
 
 @torch.no_grad()
-def test_free_running_greedy_64(eng224, G):
-    gb = G["bf16"]
+def test_teacher_forced_64_steps(eng224, G):
+    _teacher_forced(eng224, G, G["bf16"], G["fp32"], 64)
+
+
+@torch.no_grad()
+def test_teacher_forced_256_steps(eng224, G):
+    """configs[1] as BASELINE.json states it: 256 output tokens, KV length up to 544 (past the
+    12-chunk register form of the o_proj prologue's attention combine)."""
+    _teacher_forced(eng224, G, G["bf16_256"], G["fp32_256"], 256)
+
+
+@pytest.mark.parametrize("n", [64, 256])
+@torch.no_grad()
+def test_free_running_greedy(eng224, G, n):
+    gb = G["bf16"] if n == 64 else G["bf16_256"]
     ids = torch.from_numpy(gb["ids"]).cuda()
-    toks = eng224.generate(ids, _px(G, "u8_0_224"), 64, graph=True).cpu().numpy()[0]
+    toks = eng224.generate(ids, _px(G, "u8_0_224"), n, graph=True).cpu().numpy()[0]
     ref = gb["tokens"].reshape(-1)
     diff = np.nonzero(toks != ref)[0]
     if len(diff):

@@ -34,6 +34,14 @@ def main():
     fetch_b = 2.0 * 1024.0 * sum(f) / len(f)   # KiB -> B, x2 gfx950 streaming-read correction
     write_b = 1024.0 * sum(w) / len(w)
     data = json.load(open(out)) if os.path.exists(out) else {}
+    # provenance: bench.py uses the bytes only when they were measured on the same csrc sources
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import csrc_digest
+    sha = csrc_digest()
+    if data.get("csrc_sha1") != sha:
+        data = {}
+    data["csrc_sha1"] = sha
+    data["round"] = os.environ.get("PGMI_ROUND", "r02")
     data[key] = {"kernel_substring": sub, "dispatches": [len(f), len(w)], "fetch_size_kib_raw_avg": sum(f) / len(f),
                  "write_size_kib_raw_avg": sum(w) / len(w), "hbm_bytes_per_launch": fetch_b + write_b,
                  "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB->B"}

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Per-kernel evidence of one bench.py run (every config leg: 224/448 prefill, B = 1 and B = 8 decode):
+# kernel-trace stats, then MFMA-busy (SQ + GRBM), FETCH_SIZE and WRITE_SIZE in separate --pmc passes,
+# each step under its own limit; summary by tools/kernel_pmc.py.
+# usage (from the repo root, via gpurun): bash tools/gpu_kernel_pmc.sh <tag>
+set -e
+TAG=${1:-r02}
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/kpmc_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+ARGS="--steps 16 --warmup 4 --no-cpu-baseline --no-api --prefill-iters 3 --kernel-iters 18 --nokv-tokens 2"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1
+echo trace done
+timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+    --output-format csv -d $OUT/mfma -o run -- python3 $R/bench.py $ARGS > $OUT/mfma.log 2>&1
+echo mfma done
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+    python3 $R/bench.py $ARGS > $OUT/fetch.log 2>&1
+echo fetch done
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+    python3 $R/bench.py $ARGS > $OUT/write.log 2>&1
+echo write done
+python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_stats.csv $OUT/mfma/run_counter_collection.csv \
+    $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_pmc.csv > $OUT/summary.txt
+echo done
+python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
+    "k_gemv<1, 4, 1, 2, 1, true, 1>" gateup $OUT/pmc_traffic.json >> $OUT/summary.txt
+echo traffic done

@@ -186,14 +186,19 @@ int pgmi_preprocess(pgmi_ctx* ctx, const void* src_hwc, int H, int W, int out_h,
 int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* stream);
 
 /* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent
- * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-19 LDS-DMA panel tiles);
+ * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles);
  * cfg < 0 restores the automatic (measured) plan. */
 int pgmi_tune_gemm(int cfg, int split);
 
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
- * LDS-resident scores, RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
- * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); -1 restores the measured choice. */
+ * LDS-resident scores, 8 = the same with every K/V load issued up front (head_dim 256, <= 320 keys), RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
+ * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); 91, 92, 94 = K/V resident in LDS with 1, 2, 4
+ * waves of 16 query rows (short key ranges only); -1 restores the measured choice. */
 int pgmi_tune_attention(int variant);
+
+/* Diagnostics: copy the in-kernel phase stamps (100 MHz real-time counter, [slot][8 phases][64 lanes])
+ * of the last stamped diagnostic kernel variant (which = 0: prefill attention variant 9) to host. */
+int pgmi_debug_stamps(int which, long long* host, long n_words);
 
 /* Nucleus sampling, inference.py:15-24 (_sample_top_p) with inference.py:65's
  * softmax(logits / temperature) fused when temperature > 0 (temperature <= 0: x already holds

@@ -27,8 +27,7 @@ typedef short s4v_t __attribute__((ext_vector_type(4)));
 template <bool C>
 __device__ __forceinline__ short8 frag256(const uint16_t* rowp, bool valid, int kk, int lane) {
     const int k = 32 * kk + 8 * (lane >> 4);
-    if (!valid) return short8{0, 0, 0, 0, 0, 0, 0, 0};
-    return __builtin_bit_cast(short8, ldx16<C>(rowp + k));
+    return __builtin_bit_cast(short8, ldg16_sel(rowp + k, valid, rowp));
 }
 
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
@@ -50,13 +49,14 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
     for (int i = 0; i < DCH * 32 / 256; ++i) {
         const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        vr[i] = r < nk ? ldg16(vb + (long)(t0 + r) * a.v_row_stride + 8 * c) : make_uint4(0, 0, 0, 0);
+        vr[i] = ldg16_sel(vb + (long)(t0 + r) * a.v_row_stride + 8 * c, r < nk, vb);
     }
     const int qi = lane & 15;
     const bool qvalid = qi < a.G;
     const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
     const int key = t0 + wave * 16 + (lane & 15);
-    const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)key * a.k_row_stride;
+    // rows past the cache are never read: the row is clamped, its fragment zeroed (ldg16_sel)
+    const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)(key < Lk ? key : 0) * a.k_row_stride;
     short8 qf[8], kf[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<false>(krow, key < Lk, kk, lane);

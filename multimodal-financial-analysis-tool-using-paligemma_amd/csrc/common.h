@@ -20,11 +20,11 @@ __device__ __forceinline__ float bf2f(uint16_t b) {
     return __uint_as_float(((uint32_t)b) << 16);
 }
 
-// round-to-nearest-even f32 -> bf16 (inputs here are finite; a NaN stays NaN-ish)
+// round-to-nearest-even f32 -> bf16: one v_cvt_pk_bf16_f32 on gfx950 (the integer form
+// u + 0x7FFF + ((u >> 16) & 1) took four VALU ops per element; same result for finite inputs, and a
+// NaN stays a NaN -- MI355X_MICROARCH.md, correctness boundaries)
 __device__ __forceinline__ uint16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
+    return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
@@ -68,8 +68,28 @@ __device__ __forceinline__ uint4 ldg16(const void* p) {
     return *reinterpret_cast<const uint4*>(p);
 }
 
+// 16-B load whose lane may be out of range: the load is ALWAYS issued (from `safe` when !ok) and
+// the value zeroed afterwards -- a conditional load (ok ? load : 0) makes hipcc branch around the
+// load and wait vmcnt(0) for it, one dependent round trip per element (cdna_hip_programming.md
+// sec.5 "Projection GEMM at M = 256", trap (c))
+__device__ __forceinline__ uint4 ldg16_sel(const void* p, bool ok, const void* safe) {
+    const uint4 v = *reinterpret_cast<const uint4*>(ok ? p : safe);
+    return ok ? v : make_uint4(0, 0, 0, 0);
+}
+
 __device__ __forceinline__ f32x4 mfma16(const short8 a, const short8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---- diagnostics: in-kernel phase stamps (diagnostic kernel variants only; never in a product
+// launch).  Every lane of wave 0 stores the 100 MHz real-time counter at a phase boundary into
+// buf[(slot * kStampPhases + phase) * 64 + lane] with a vector store (divergent address); each
+// translation unit that stamps owns its buffer and a host read-back (pgmi_debug_stamps).
+constexpr int kStampPhases = 8, kStampSlots = 512;
+constexpr long kStampWords = (long)kStampSlots * kStampPhases * 64;
+__device__ __forceinline__ void stamp_to(long long* buf, int slot, int phase) {
+    if (threadIdx.x < 64 && slot < kStampSlots)
+        buf[((long)slot * kStampPhases + phase) * 64 + threadIdx.x] = (long long)wall_clock64();
 }
 
 }  // namespace pgmi

@@ -1074,13 +1074,20 @@ int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* strea
 }
 
 int pgmi_tune_gemm(int cfg, int split) {
-    if (cfg > 23 || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
+    if (cfg > 29 || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
     gemm_force_plan(cfg, split);
     return 0;
 }
 
+int pgmi_debug_stamps(int which, long long* host, long n_words) {
+    if (!host || n_words < 0) return fail(PGMI_E_ARG, "bad argument");
+    if (which != 0) return fail(PGMI_E_ARG, "unknown stamp buffer");
+    if (attn_debug_stamps(host, n_words)) return fail(PGMI_E_HIP, "stamp read-back failed");
+    return 0;
+}
+
 int pgmi_tune_attention(int variant) {
-    static const int ok[] = {-1, 0, 41, 42, 21, 22, 44, 24};
+    static const int ok[] = {-1, 0, 8, 9, 41, 42, 21, 22, 44, 24, 91, 92, 94};
     for (int v : ok)
         if (v == variant) {
             attention_force_variant(variant);

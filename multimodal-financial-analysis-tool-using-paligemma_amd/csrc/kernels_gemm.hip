@@ -430,7 +430,14 @@ enum Cfg : int {
     Q352w = 21,    // 2x4 waves, TM 11, BN 128, 2 slots
     Q256w = 22,    // 2x4 waves, TM 8,  BN 128, 3 slots
     Q288x256 = 23, // 2x4 waves, TM 9,  BN 256, 2 slots
-    kNumCfg = 24,
+    // shallow rings (2-3 workgroups per CU: more k-tiles in flight per CU for the small GEMMs)
+    P64x64s3 = 24, // TM 2, BN 64, 3 slots
+    P64x64s4 = 25, // TM 2, BN 64, 4 slots
+    P32x64s4 = 26, // TM 1, BN 64, 4 slots
+    P64x32s4 = 27, // TM 2, BN 32, 4 slots
+    P96x64s4 = 28, // TM 3, BN 64, 4 slots (M = 288 = 3 x 96)
+    P96x64s3 = 29, // TM 3, BN 64, 3 slots
+    kNumCfg = 30,
 };
 
 struct Plan {
@@ -451,8 +458,8 @@ void gemm_force_plan(int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -464,16 +471,17 @@ static Plan choose(int M, int N, int K, bool dual) {
     // projections want full-M panels that read each weight byte once.
     struct Entry { int M, N, K; bool dual; Cfg cfg; int split; };
     static const Entry table[] = {
-        {288, 2560, 2048, false, P64x64, 1},    // text q|k|v            11.5 us
-        {288, 2048, 2048, false, P64x64, 1},    // text o_proj           13.0 us
+        // round 2 (tools/gemm_sweep.py, shallow-ring configs 24-29: 2-3 workgroups per CU)
+        {288, 2560, 2048, false, P64x64s4, 1},  // text q|k|v            11.1 us
+        {288, 2048, 2048, false, P64x64s3, 1},  // text o_proj           12.8 us
         {288, 16384, 2048, true, Q288w, 1},     // text gate|up (GeGLU)  44 us
         {288, 2048, 16384, false, P288n, 8},    // text down             38 us
-        {256, 3456, 1152, false, P64x64, 1},    // vision q|k|v          10.1 us
-        {256, 1152, 1152, false, P64x64, 1},    // vision out_proj        9.9 us
-        {256, 4304, 1152, false, P128w, 3},     // vision fc1            18.5 us
-        {256, 1152, 4304, false, P64x64, 3},    // vision fc2            15.0 us
+        {256, 3456, 1152, false, P64x32s4, 1},  // vision q|k|v           9.9 us
+        {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        7.8 us
+        {256, 4304, 1152, false, P64x32s4, 1},  // vision fc1 (+GELU)    13.9 us (was split 3 + epilogue kernel)
+        {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            14.9 us
         {256, 1152, 640, false, P64x64, 1},     // patch embedding        7.5 us
-        {256, 2048, 1152, false, P64x64, 1},    // multimodal projector   9.5 us
+        {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
         {1056, 2560, 2048, false, P128w, 1},    // 448 px text q|k|v     23.7 us
         {1056, 2048, 2048, false, P288n, 2},    // 448 px text o_proj    28.2 us
         {1056, 16384, 2048, true, Q352w, 1},    // 448 px gate|up       147 us
@@ -481,8 +489,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {1024, 4304, 1152, false, Q352w, 2},    // 448 px vision fc1     34 us
         {1024, 3456, 1152, false, P128w, 1},    // 448 px vision q|k|v   23.3 us
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
@@ -610,6 +618,12 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case Q352w: P8_(2, 11, 2, 2); break;
         case Q256w: P8_(2, 8, 2, 3); break;
         case Q288x256: P8_(2, 9, 4, 2); break;
+        case P64x64s3: P_(2, 2, 2, 3); break;
+        case P64x64s4: P_(2, 2, 2, 4); break;
+        case P32x64s4: P_(2, 1, 2, 4); break;
+        case P64x32s4: P_(2, 2, 1, 4); break;
+        case P96x64s4: P_(2, 3, 2, 4); break;
+        case P96x64s3: P_(2, 3, 2, 3); break;
         default: break;
     }
 #undef P_

@@ -79,6 +79,7 @@ SIGNATURES = {
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),
     "pgmi_tune_attention": (i32, [i32]),
+    "pgmi_debug_stamps": (i32, [i32, vp, ctypes.c_long]),
     "pgmi_sample_top_p": (i32, [vp, vp, i32, i32, f32, f32, vp, vp, vp, vp]),
     "pgmi_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]),
     "pgmi_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, f32, vp, vp]),

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--cfgs", default="0,2,4,5,6,7,8,9,10,11")
     ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cold", action="store_true",
+                    help="rotate over distinct weight copies (> 256 MiB in all) so every call reads its weights "
+                         "from HBM, as the layer loop of a forward does")
     args = ap.parse_args()
     e = Engine(W.small_config(1, 1, 1024), max_batch=1, max_seq=320, max_kv=512)
     e.fill_synthetic(1, W.init_policy)
@@ -46,13 +49,18 @@ def main():
         M, Nn, K, epi = SHAPES[name]
         A = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         Wt = ((torch.rand(Nn * (2 if epi == 7 else 1), K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        nw = max(1, -(-(320 << 20) // (Wt.numel() * 2))) if args.cold else 1
+        Ws = [Wt] + [Wt.clone() for _ in range(nw - 1)]
+        wi = [0]
         bias = torch.randn(Nn, device="cuda").to(torch.bfloat16)
         res = torch.randn(M, Nn, device="cuda").to(torch.bfloat16)
         out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
         flops = 2.0 * M * Nn * K * (2 if epi == 7 else 1)
 
         def run(st=None):
-            N.check(lib.pgmi_op_gemm(e.ctx, A.data_ptr(), Wt.data_ptr(), M, Nn, K, epi, bias.data_ptr(),
+            w = Ws[wi[0] % nw]
+            wi[0] += 1
+            N.check(lib.pgmi_op_gemm(e.ctx, A.data_ptr(), w.data_ptr(), M, Nn, K, epi, bias.data_ptr(),
                                      res.data_ptr(), out.data_ptr(), st or s))
 
         N.check(lib.pgmi_tune_gemm(4 if M > 288 else 5, 1))
@@ -76,7 +84,7 @@ def main():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     cs = torch.cuda.current_stream().cuda_stream
-                    for _ in range(args.iters):
+                    for _ in range(max(args.iters, nw)):
                         run(cs)
                 g.replay()
                 torch.cuda.synchronize()
@@ -85,7 +93,7 @@ def main():
                 g.replay()
                 t1.record()
                 t1.synchronize()
-                us = t0.elapsed_time(t1) * 1e3 / args.iters
+                us = t0.elapsed_time(t1) * 1e3 / max(args.iters, nw)
                 del g
                 rows.append((us, cfg, split, err))
         N.check(lib.pgmi_tune_gemm(-1, 0))

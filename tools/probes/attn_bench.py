@@ -19,9 +19,11 @@ eng = Engine(W.small_config(vision_layers=1, text_layers=1, vocab=1024), max_bat
 shapes = [("siglip224", 256, 16, 16, 72), ("siglip448", 1024, 16, 16, 72),
           ("gemma224", 288, 8, 1, 256), ("gemma448", 1056, 8, 1, 256)]
 torch.manual_seed(0)
-variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 41, 42, 21, 22, 44, 24]
+variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 8, 41, 42, 21, 22, 44, 24, 91, 92, 94]
 for var, (name, L, H, Hkv, d) in [(v, sh) for sh in shapes for v in variants]:
     if var in (44, 24) and d != 72:
+        continue
+    if (var >= 91 and name != "siglip224") or (var == 8 and name != "gemma224"):
         continue
     NN.check(eng.lib.pgmi_tune_attention(var))
     scale = d ** -0.5
@@ -37,14 +39,23 @@ for var, (name, L, H, Hkv, d) in [(v, sh) for sh in shapes for v in variants]:
     for _ in range(3):
         run()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # GPU time: the calls replayed from a captured graph (ctypes host launches would floor them)
     n = 20
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream().cuda_stream
+        for _ in range(n):
+            run()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(n):
-        run()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / n * 1e3
+    del g
+    s = NN.stream_handle()
     qh = q.float().transpose(1, 2)
     kh = k.float().transpose(1, 2).repeat_interleave(H // Hkv, 1)
     vh = v.float().transpose(1, 2).repeat_interleave(H // Hkv, 1)

@@ -186,7 +186,7 @@ int pgmi_preprocess(pgmi_ctx* ctx, const void* src_hwc, int H, int W, int out_h,
 int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* stream);
 
 /* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent
- * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles);
+ * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles, 30-35 warp-specialised panel tiles);
  * cfg < 0 restores the automatic (measured) plan. */
 int pgmi_tune_gemm(int cfg, int split);
 

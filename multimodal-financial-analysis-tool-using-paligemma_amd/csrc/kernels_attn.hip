@@ -206,8 +206,8 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     constexpr int VPT = (CHK * I::CH + 255) / 256;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int LkP = (a.Lk + 31) & ~31;
-    uint16_t* S = reinterpret_cast<uint16_t*>(smem_raw);  // [16][LkP] bf16 scores, then P in place
-    uint16_t* Vl = S + 16 * LkP;                          // [2][CHK][VS]
+    uint16_t* S = reinterpret_cast<uint16_t*>(smem_raw);  // [16][LkP] bf16 P
+    uint16_t* Vl = S + 16 * LkP;                          // [2][CHK][VS], then [2][4][16] fp32 row stats
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.z, kvh = blockIdx.y;
@@ -247,38 +247,72 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         }
     if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 1);
 
-    // ---- phase 1: S = bf16(bf16(Q K^T) * scale)
+    // ---- phase 1: s = bf16(bf16(Q K^T) * scale), kept in registers: lane (g, li) holds rows 4g + r
+    // of keys 16 t + li for this wave's tiles t = wave + 4 j
+    const int g = lane >> 4, li = lane & 15;
+    float sc[MAXT][4];
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
         const int t = wave + 4 * j;
-        if (t < ntile) {
-            const int key = t * 16 + (lane & 15);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int key = t * 16 + li;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kk = 0; kk < I::KS; ++kk) acc = mfma16(qf[kk], kf[j][kk], acc);
+        for (int kk = 0; kk < I::KS; ++kk) acc = mfma16(qf[kk], kf[j][kk], acc);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = (lane >> 4) * 4 + r;
-                S[row * LkP + key] = key < a.Lk ? f2bf(rbf(rbf(acc[r]) * a.scale)) : (uint16_t)0xFF80;  // -inf
-            }
-        }
+        for (int r = 0; r < 4; ++r) sc[j][r] = (t < ntile && key < a.Lk) ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
+    }
+    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 2);
+    // ---- phase 2: exact softmax per row: max and sum of exp over the row's keys (lane, then the 16
+    // lanes of a row group, then the 4 waves in a fixed order), p = bf16(exp(s - max) / sum) -> LDS
+    float* red = reinterpret_cast<float*>(Vl + 2 * CHK * VS);  // [2][4 waves][16 rows]
+    float mx[4], sm[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        mx[r] = sc[0][r];
+#pragma unroll
+        for (int j = 1; j < MAXT; ++j) mx[r] = fmaxf(mx[r], sc[j][r]);
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+    if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wave * 16 + 4 * g + r] = mx[r];
     }
     __syncthreads();
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 2);
-    // ---- phase 2: exact softmax per row (fp32 from the bf16 scores), P = bf16(p) in place
-    for (int row = wave; row < 16; row += 4) {
-        float m = -INFINITY;
-        for (int t = lane; t < a.Lk; t += 64) m = fmaxf(m, bf2f(S[row * LkP + t]));
-        m = wave_max(m);
-        float sum = 0.f;
-        for (int t = lane; t < a.Lk; t += 64) sum += expf(bf2f(S[row * LkP + t]) - m);
-        sum = wave_sum(sum);
-        for (int t = lane; t < LkP; t += 64)
-            S[row * LkP + t] = t < a.Lk ? f2bf(expf(bf2f(S[row * LkP + t]) - m) / sum) : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r;
+        mx[r] = fmaxf(fmaxf(red[row], red[16 + row]), fmaxf(red[32 + row], red[48 + row]));
+        sm[r] = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXT; ++j) {
+            sc[j][r] = sc[j][r] == -INFINITY ? 0.f : expf(sc[j][r] - mx[r]);
+            sm[r] += sc[j][r];
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm[r] += __shfl_xor(sm[r], o, 64);
+    if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[64 + wave * 16 + 4 * g + r] = sm[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r;
+        const float L = ((red[64 + row] + red[80 + row]) + red[96 + row]) + red[112 + row];
+#pragma unroll
+        for (int j = 0; j < MAXT; ++j) {
+            const int key = (wave + 4 * j) * 16 + li;
+            if (key < LkP) S[row * LkP + key] = key < a.Lk ? f2bf(sc[j][r] / L) : 0;
+        }
     }
     if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 3);
     // ---- phase 3: O = bf16(P V), V chunks staged from registers into two LDS buffers
-    const int g = lane >> 4, li = lane & 15;
     f32x4 oacc[(I::CT + 3) / 4];
 #pragma unroll
     for (int c = 0; c < (I::CT + 3) / 4; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -820,7 +854,7 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
     }
     if ((v == 8 || v == 9) && head_dim == 256 && a.Lk <= 320) {
         // 16 query rows per workgroup, every K/V load issued up front (Lk <= 320)
-        const size_t lds = (size_t)16 * ((a.Lk + 31) & ~31) * 2 + (size_t)2 * 32 * (256 + 16) * 2;
+        const size_t lds = (size_t)16 * ((a.Lk + 31) & ~31) * 2 + (size_t)2 * 32 * (256 + 16) * 2 + 2 * 4 * 16 * 4;
         dim3 grid((a.Lq * a.G + 15) / 16, a.n_kv, a.B);
         if (v == 9) hipLaunchKernelGGL((k_attn_full_pre<256, 5, 10, true>), grid, dim3(256), lds, s, a);  // stamped
         else hipLaunchKernelGGL((k_attn_full_pre<256, 5, 10>), grid, dim3(256), lds, s, a);

@@ -402,6 +402,166 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
         }
 }
 
+// ---------------------------------------------------------------- warp-specialised panel GEMM
+// k_gemm_p's tiles, LDS image and fragment reads, with the two roles split over the waves of the
+// workgroup: NW compute waves (the WM x WN wave grid) only read fragments and run MFMAs; LW loader
+// waves only issue the LDS-DMA of the ring (k_gemm_p's waves issue both, and an LDS-DMA issue stalls
+// its wave for ~60-185 cycles per KiB beside MFMAs -- at the prefill's M = 256..288 panels that
+// stall, not the matrix pipe, set the k-step time).  One raw s_barrier per k-tile: before barrier t
+// every loader has counted its own DMA of tile t as landed (vmcnt), after it the loaders refill the
+// slot of tile t-1 (whose fragments every compute wave read before reaching barrier t).
+template <int NW, int WM, int TM, int TN, int NB, int ST, int LW, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __restrict__ A, int lda,
+                                                          const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                          int kt_per_split, EpiArgs ea, float* __restrict__ ws,
+                                                          long up_off, int n_mt, int n_nt) {
+    constexpr int WN = NW / WM;
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
+    constexpr int PCS = APC + BPC;
+    constexpr int GPW = (PCS + LW - 1) / LW;        // LDS-DMA instructions per loader wave per k-tile
+    constexpr int ABYTES = BM * 128;
+    constexpr int SBYTES = (BM + NB * BN) * 128;
+    static_assert(ST >= 2, "ring of at least two slots");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_w[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.x;
+    int mt, nt;
+    if ((n_nt & 7) == 0) {
+        const int j = b >> 3;
+        mt = j % n_mt;
+        nt = (j / n_mt) * 8 + (b & 7);
+    } else {
+        mt = b % n_mt;
+        nt = b / n_mt;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int nkt_total = (K + 63) / 64;
+    const int kt0 = blockIdx.y * kt_per_split;
+    int kt1 = kt0 + kt_per_split;
+    if (kt1 > nkt_total) kt1 = nkt_total;
+    const int nkt = kt1 > kt0 ? kt1 - kt0 : 0;
+
+    if (wave >= NW) {
+        // ---------------- loader wave
+        const int lw = wave - NW;
+        const uint16_t* src[GPW];
+        int gk[GPW], loff[GPW];
+        const int prow = lane >> 3, pchunk = lane & 7;
+#pragma unroll
+        for (int i = 0; i < GPW; ++i) {
+            int p = lw + LW * i;
+            if (p >= PCS) p -= PCS;  // padding: repeat a piece (same bytes to the same LDS address)
+            loff[i] = p * 1024;
+            int row;
+            const uint16_t* base;
+            long ld;
+            if (p < APC) {
+                row = m0 + p * 8 + prow;
+                if (row > M - 1) row = M - 1;
+                base = A;
+                ld = lda;
+            } else {
+                const int q = p - APC;
+                const int bo = q / (BN / 8);
+                row = n0 + (q % (BN / 8)) * 8 + prow;
+                if (row > N - 1) row = N - 1;
+                base = W + bo * up_off;
+                ld = ldw;
+            }
+            gk[i] = (pchunk ^ (row & 7)) * 8;
+            src[i] = base + (long)row * ld + gk[i];
+        }
+        const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+        auto issue = [&](int kt, int slot) {
+            const int kel = kt * 64;
+            if (kel + 64 <= K) {
+#pragma unroll
+                for (int i = 0; i < GPW; ++i)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
+                                                     (__attribute__((address_space(3))) void*)(smem_w + slot * SBYTES + loff[i]),
+                                                     16, 0, 0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < GPW; ++i) {
+                    const uint16_t* g = (kel + gk[i] < K) ? src[i] + kel : zero;
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
+                                                     (__attribute__((address_space(3))) void*)(smem_w + slot * SBYTES + loff[i]),
+                                                     16, 0, 0);
+                }
+            }
+        };
+#pragma unroll
+        for (int sI = 0; sI < ST - 1; ++sI)
+            if (sI < nkt) issue(kt0 + sI, sI);
+        int slot_next = ST - 1;  // slot of tile t + ST - 1
+        for (int t = 0; t < nkt; ++t) {
+            const int issued = (nkt < t + ST - 1) ? nkt : t + ST - 1;
+            vm_wait_tiles<GPW, ST - 2>(issued - t - 1);  // tile t landed
+            __builtin_amdgcn_s_barrier();
+            if (t + ST - 1 < nkt) issue(kt0 + t + ST - 1, slot_next);
+            slot_next = slot_next + 1 == ST ? 0 : slot_next + 1;
+        }
+        return;
+    }
+
+    // ---------------- compute wave
+    const int wm = wave / WN, wn = wave % WN;
+    f32x4 acc[NB][TM][TN];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[bb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int swz = lane & 7;
+    const int arow0 = (wm * TM * 16 + (lane & 15)) * 128;
+    const int brow0 = ABYTES + (wn * TN * 16 + (lane & 15)) * 128;
+    short8 fa[TM], fb[NB][TN];
+    int slot = 0;
+    for (int t = 0; t < nkt; ++t) {
+        __builtin_amdgcn_s_barrier();  // tile t is in slot `slot`
+        const uint8_t* sb = smem_w + slot * SBYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = (((kk * 4) + (lane >> 4)) ^ swz) << 4;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const short8*>(sb + arow0 + i * 16 * 128 + ch);
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    fb[bb][j] = *reinterpret_cast<const short8*>(sb + brow0 + (bb * BN + j * 16) * 128 + ch);
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[bb][i][j] = mfma16(fa[i], fb[bb][j], acc[bb][i][j]);
+        }
+        slot = slot + 1 == ST ? 0 : slot + 1;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
+                if (m < M && n < N) {
+                    if constexpr (SPLIT) {
+                        ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
+                    } else {
+                        epi_store<EPI>(ea, m, n, acc[0][i][j][r], NB == 2 ? acc[NB - 1][i][j][r] : 0.f);
+                    }
+                }
+            }
+        }
+}
+
 // Tile configurations (wave grid, per-wave MFMA tiles).  BM = WGM*TM*16, BN = WGN*TN*16.
 enum Cfg : int {
     C288x64 = 0,   // 6x1 waves, 3x4 tiles  (text rows: M = 288 = 18 x 16)
@@ -437,7 +597,14 @@ enum Cfg : int {
     P64x32s4 = 27, // TM 2, BN 32, 4 slots
     P96x64s4 = 28, // TM 3, BN 64, 4 slots (M = 288 = 3 x 96)
     P96x64s3 = 29, // TM 3, BN 64, 3 slots
-    kNumCfg = 30,
+    // warp-specialised (k_gemm_w): compute waves + 4 LDS-DMA loader waves
+    W288w = 30,    // 2x4 compute waves, TM 9,  BN 128, 3 slots
+    W288n = 31,    // 2x4 compute waves, TM 9,  BN 64,  3 slots
+    W64x64 = 32,   // 2x2 compute waves, TM 2,  BN 64,  6 slots
+    W352w = 33,    // 2x4 compute waves, TM 11, BN 128, 2 slots
+    W128x128 = 34, // 2x4 compute waves, TM 4,  BN 128, 4 slots
+    W128x64 = 35,  // 2x2 compute waves, TM 4,  BN 64,  5 slots
+    kNumCfg = 36,
 };
 
 struct Plan {
@@ -458,8 +625,8 @@ void gemm_force_plan(int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -471,26 +638,27 @@ static Plan choose(int M, int N, int K, bool dual) {
     // projections want full-M panels that read each weight byte once.
     struct Entry { int M, N, K; bool dual; Cfg cfg; int split; };
     static const Entry table[] = {
-        // round 2 (tools/gemm_sweep.py, shallow-ring configs 24-29: 2-3 workgroups per CU)
-        {288, 2560, 2048, false, P64x64s4, 1},  // text q|k|v            11.1 us
-        {288, 2048, 2048, false, P64x64s3, 1},  // text o_proj           12.8 us
-        {288, 16384, 2048, true, Q288w, 1},     // text gate|up (GeGLU)  44 us
-        {288, 2048, 16384, false, P288n, 8},    // text down             38 us
-        {256, 3456, 1152, false, P64x32s4, 1},  // vision q|k|v           9.9 us
-        {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        7.8 us
-        {256, 4304, 1152, false, P64x32s4, 1},  // vision fc1 (+GELU)    13.9 us (was split 3 + epilogue kernel)
-        {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            14.9 us
+        // round 2: tools/gemm_sweep.py --cold (every call reads its weights from HBM, as the layer
+        // loop does); W* = warp-specialised (k_gemm_w), P*s* = shallow rings
+        {288, 2560, 2048, false, W64x64, 1},    // text q|k|v            10.8 us
+        {288, 2048, 2048, false, W64x64, 1},    // text o_proj           12.4 us
+        {288, 16384, 2048, true, W288w, 1},     // text gate|up (GeGLU)  44.6 us (was 55.8 cold)
+        {288, 2048, 16384, false, W288n, 8},    // text down             37.7 us
+        {256, 3456, 1152, false, W64x64, 1},    // vision q|k|v          10.7 us
+        {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        8.9 us
+        {256, 4304, 1152, false, P64x32s4, 1},  // vision fc1 (+GELU)    16.4 us (was split 3 + epilogue kernel)
+        {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            18.4 us
         {256, 1152, 640, false, P64x64, 1},     // patch embedding        7.5 us
         {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
         {1056, 2560, 2048, false, P128w, 1},    // 448 px text q|k|v     23.7 us
         {1056, 2048, 2048, false, P288n, 2},    // 448 px text o_proj    28.2 us
-        {1056, 16384, 2048, true, Q352w, 1},    // 448 px gate|up       147 us
-        {1056, 2048, 16384, false, Q352w, 4},   // 448 px down           92 us
+        {1056, 16384, 2048, true, W352w, 1},    // 448 px gate|up       153.8 us (was 180.9 cold)
+        {1056, 2048, 16384, false, W288w, 4},   // 448 px down           85.1 us (was 99.5 cold)
         {1024, 4304, 1152, false, Q352w, 2},    // 448 px vision fc1     34 us
         {1024, 3456, 1152, false, P128w, 1},    // 448 px vision q|k|v   23.3 us
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
@@ -594,6 +762,45 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
 }
 
+// warp-specialised launcher: as launch_p, NW compute waves (grid WM x NW/WM) + LW loader waves
+template <int NW, int WM, int TM, int TNW, int ST, int LW, int EPI>
+static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                     const EpiArgs& ea, float* ws, int split, long up_off) {
+    constexpr bool DUAL = (EPI == EPI_GEGLU);
+    constexpr int NB = DUAL ? 2 : 1;
+    constexpr int TN = DUAL ? (TNW >= 2 ? TNW / 2 : 1) : TNW;
+    constexpr int BM = WM * TM * 16, BN = (NW / WM) * TN * 16;
+    constexpr size_t lds = (size_t)ST * (BM + NB * BN) * 128;
+    static_assert(lds <= 163840, "LDS ring exceeds 160 KiB");
+    constexpr int EK = EPI < 0 ? EPI_STORE : EPI;
+    const int nkt = (K + 63) / 64;
+    const int per = (nkt + split - 1) / split;
+    const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
+    dim3 grid(n_mt * n_nt, split);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    const dim3 block(64 * (NW + LW));
+    if (EPI < 0 || split > 1) {
+        hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+                           per, ea, ws, up_off, n_mt, n_nt);
+        if (EPI >= 0) {
+            long total4 = ((long)M * N + 3) / 4;
+            long blocks = (total4 + 255) / 256;
+            if (blocks > 4096) blocks = 4096;
+            hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
+        }
+    } else {
+        hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+                           per, ea, ws, up_off, n_mt, n_nt);
+    }
+}
+
 template <int EPI>
 static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                         const EpiArgs& ea, float* ws, const Plan& p, long up_off) {
@@ -624,6 +831,12 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case P64x32s4: P_(2, 2, 1, 4); break;
         case P96x64s4: P_(2, 3, 2, 4); break;
         case P96x64s3: P_(2, 3, 2, 3); break;
+        case W288w: launch_w<8, 2, 9, 2, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W288n: launch_w<8, 2, 9, 1, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W64x64: launch_w<4, 2, 2, 2, 6, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W352w: launch_w<8, 2, 11, 2, 2, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W128x128: launch_w<8, 2, 4, 2, 4, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W128x64: launch_w<4, 2, 4, 2, 5, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         default: break;
     }
 #undef P_

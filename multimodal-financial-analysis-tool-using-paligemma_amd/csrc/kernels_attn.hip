@@ -827,7 +827,7 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
     // K/V-resident kernel (variants 91, 92, 94: 1, 2, 4 waves of 16 query rows per workgroup)
     const bool lds_fits = head_dim == 72 ? attn_lds_bytes<72>(a.Lk) <= 160 * 1024
                                          : attn_lds_bytes<256>(a.Lk) <= 160 * 1024;
-    if (v < 0 && head_dim == 72 && lds_fits) v = 94;
+    // (opt-in only: at SigLIP 224 variant 94 measured 15.7 us against 10.7 for RG2xKSPL4)
     if (v >= 91 && v <= 94 && lds_fits) {
         if (head_dim == 72) {
             if (v == 91) launch_attn_lds<72, 1>(s, a);

@@ -656,6 +656,16 @@ static Plan choose(int M, int N, int K, bool dual) {
         {1056, 2048, 16384, false, W288w, 4},   // 448 px down           85.1 us (was 99.5 cold)
         {1024, 4304, 1152, false, Q352w, 2},    // 448 px vision fc1     34 us
         {1024, 3456, 1152, false, P128w, 1},    // 448 px vision q|k|v   23.3 us
+        // configs[3]: 8 images per GPU as one batch (vision 2048 rows, text 2304 rows), cold sweep
+        {2048, 3456, 1152, false, W288w, 1},    // vision q|k|v          31.2 us (was 46.8)
+        {2048, 1152, 1152, false, W128x128, 1}, // vision out_proj       22.3 us (was 31.6)
+        {2048, 4304, 1152, false, W352w, 1},    // vision fc1            48.6 us (was 91.5)
+        {2048, 1152, 4304, false, W288w, 2},    // vision fc2            47.3 us (was 72.2)
+        {2048, 2048, 1152, false, W128x128, 1}, // projector             19.1 us (was 23.8)
+        {2304, 2560, 2048, false, W288w, 1},    // text q|k|v            32.8 us (was 48.3)
+        {2304, 2048, 2048, false, W288n, 1},    // text o_proj           35.4 us (was 62.1)
+        {2304, 16384, 2048, true, W288w, 1},    // text gate|up         308.9 us (was 377.4)
+        {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)
     };
     static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
     static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
@@ -669,8 +679,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         if (K >= 8192) return mk(P64x64, 8);
     }
     // other shapes (batched prefill: M = B x 256 / 288 rows; other image sizes)
-    if (dual) return mk(M <= 256 ? Q256w : M <= 288 ? Q288w : Q352w, 1);
-    if (K >= 8192) return mk(M <= 288 ? P288n : P288w, M <= 288 ? 8 : 4);
+    if (dual) return mk(M <= 288 || M >= 2048 ? W288w : W352w, 1);
+    if (K >= 8192) return mk(M <= 288 ? W288n : W288w, M <= 288 ? 8 : M <= 1056 ? 4 : 2);
     const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (t64 <= 256) return mk(P64x64, 1);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);

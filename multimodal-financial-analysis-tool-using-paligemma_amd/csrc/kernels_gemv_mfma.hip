@@ -62,8 +62,11 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
     float ss[MF_MAXB];
 #pragma unroll
     for (int b = 0; b < MF_MAXB; ++b) ss[b] = 0.f;
-    const bool one = (K == nt * 8);  // K = 2048, 256 threads: one chunk per thread, norm weights fetched now
-    const uint4 wv0 = (one && a.norm_w) ? ldg16(a.norm_w + tid * 8) : make_uint4(0, 0, 0, 0);
+    // K <= 8 x threads (K = 2048 at 256 or 512 threads): one chunk per thread, and its norm weights are
+    // fetched with the rows (one round trip, not a second one after the reduction)
+    const bool one = (K <= nt * 8);
+    const bool has = tid * 8 < K;
+    const uint4 wv0 = (one && a.norm_w) ? ldg16(a.norm_w + (has ? tid * 8 : 0)) : make_uint4(0, 0, 0, 0);
     for (int c = tid * 8; c < K; c += nt * 8) {
         uint4 v[MF_MAXB];
 #pragma unroll
@@ -149,6 +152,17 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     };
     int grp = blockIdx.x;
     if (grp < n_groups) issue(grp);
+    // RoPE operands of this workgroup's first group, fetched with the weight stream (the epilogue
+    // would otherwise pay their round trip after the reduction)
+    float cs0 = 0.f, sn0 = 0.f;
+    if constexpr (MODE == GV_QKV) {
+        int p0 = a.st->position;
+        p0 = p0 < 0 ? 0 : (p0 > a.max_pos - 1 ? a.max_pos - 1 : p0);
+        const int d0 = (grp * 16 + n) & 127;
+        cs0 = bf2f(a.cosT[(long)p0 * 128 + d0]);
+        sn0 = bf2f(a.sinT[(long)p0 * 128 + d0]);
+    }
+    const int grp0 = grp;
 
     // ---- activations: this wave's K slice, MFMA A layout (row b = lane & 15)
     short8 xf[NKB][4];
@@ -234,8 +248,8 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 const float x0 = rbf(acc[0][r]), x1 = rbf(acc[1][r]);
                 const int nh = a.I;
                 if (hh < nh + a.nkv) {
-                    const float c = bf2f(a.cosT[(long)pos * 128 + d]);
-                    const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
+                    const float c = cur == grp0 ? cs0 : bf2f(a.cosT[(long)pos * 128 + d]);
+                    const float sn = cur == grp0 ? sn0 : bf2f(a.sinT[(long)pos * 128 + d]);
                     const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
                     const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sn));
                     uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256

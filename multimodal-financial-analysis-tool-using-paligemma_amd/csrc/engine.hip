@@ -1093,6 +1093,12 @@ int pgmi_tune_attention(int variant) {
             attention_force_variant(variant);
             return 0;
         }
+    // tiled kernel with a register prefetch of PD = 2..4 tiles: 100 * PD + (41, 42, 21, 22, 44, 24)
+    const int pd = variant / 100, rk = variant % 100;
+    if (pd >= 2 && pd <= 4 && (rk == 41 || rk == 42 || rk == 21 || rk == 22 || rk == 44 || rk == 24)) {
+        attention_force_variant(variant);
+        return 0;
+    }
     return fail(PGMI_E_ARG, "unknown attention variant");
 }
 

@@ -141,10 +141,8 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         if constexpr (DEPTH == 2) issue(S1{}, ub + stride);
         asm volatile("" ::: "memory");  // keep the weight stream ahead of the norm (no sinking past it)
     } else {
-        if (ub < bend) issue(S0{}, ub);
-        if constexpr (DEPTH == 2) {
-            if (ub + stride < bend) issue(S1{}, ub + stride);
-        }
+        issue(S0{}, ub);
+        if constexpr (DEPTH == 2) issue(S1{}, ub + stride);
         load_x();
     }
 
@@ -296,8 +294,13 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
     for (int b = 0; b < B; ++b) { best[b] = -INFINITY; besti[b] = 0x7fffffff; }
 
-    auto step = [&](auto slot) {
+    // ISSUE: start the stream of group +DEPTH in this step.  The loop below peels the last group
+    // (DEPTH 1) so the in-loop issue is unconditional: behind a branch the compiler cannot count
+    // the loads in flight and waits vmcnt(0) -- for the next group's stream -- at the epilogue's
+    // residual read
+    auto step = [&](auto slot, auto issue_next) {
         constexpr int SL = decltype(slot)::value;
+        constexpr bool ISSUE = decltype(issue_next)::value;
         // epilogue operands of this group (residual h, RoPE cos/sin), queued behind its weights
         float pre[RPW][B][2];
 #pragma unroll
@@ -338,7 +341,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         ub += stride;
         bb += stride;
         // the stream of group +DEPTH starts before this group's epilogue, into the freed set
-        if (ub + (DEPTH - 1) * stride < bend) issue(slot, ub + (DEPTH - 1) * stride);
+        if constexpr (ISSUE) {
+            if constexpr (DEPTH == 1) issue(slot, ub + (DEPTH - 1) * stride);
+            else if (ub + (DEPTH - 1) * stride < bend) issue(slot, ub + (DEPTH - 1) * stride);
+        }
 
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
@@ -421,11 +427,16 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             }
         }
     };
-    while (bb < bend) {
-        step(S0{});
-        if constexpr (DEPTH == 2) {
+    using Yes = std::true_type;
+    using No = std::false_type;
+    if constexpr (DEPTH == 1) {
+        while (bb + stride < bend) step(S0{}, Yes{});  // a next group exists: stream it
+        if (bb < bend) step(S0{}, No{});
+    } else {
+        while (bb < bend) {
+            step(S0{}, Yes{});
             if (bb >= bend) break;
-            step(S1{});
+            step(S1{}, Yes{});
         }
     }
 

@@ -39,6 +39,19 @@ __device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool valid, in
 
 typedef s4v_t s4v;
 
+// output rows of the C map (16x16x32: lane holds rows 4g + r, r < 4, of its 16-row group): the
+// four row pointers are resolved once (row -> (position, head) takes a division by G), so the
+// per-element stores are a plain offset (nullptr: row past the end)
+__device__ __forceinline__ void attn_out_rows(const AttnArgs& a, int b, int kvh, int i0, int nrows,
+                                              uint16_t* (&orow)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r;
+        const int pos = i / a.G, head = kvh * a.G + i % a.G;
+        orow[r] = i < nrows ? a.o + b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride : nullptr;
+    }
+}
+
 __device__ long long g_attn_stamps[kStampWords];  // diagnostic stamps of the STAMP kernel variants
 
 int attn_debug_stamps(long long* host, long n_words) {
@@ -174,6 +187,8 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
             }
         }
     }
+    uint16_t* orow[4];
+    attn_out_rows(a, b, kvh, row0 + (lane >> 4) * 4, nrows, orow);
 #pragma unroll
     for (int c = 0; c < (I::CT + 3) / 4; ++c) {
         const int ct = wave + 4 * c;
@@ -181,12 +196,8 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
         const int d = ct * 16 + (lane & 15);
         if (d >= HD) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = row0 + (lane >> 4) * 4 + r;
-            if (i >= nrows) continue;
-            const int pos = i / a.G, head = kvh * a.G + i % a.G;
-            a.o[b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + d] = f2bf(oacc[c][r]);
-        }
+        for (int r = 0; r < 4; ++r)
+            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
     }
 }
 
@@ -347,6 +358,8 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         }
     }
     if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 4);
+    uint16_t* orow[4];
+    attn_out_rows(a, b, kvh, row0 + (lane >> 4) * 4, nrows, orow);
 #pragma unroll
     for (int c = 0; c < (I::CT + 3) / 4; ++c) {
         const int ct = wave + 4 * c;
@@ -354,12 +367,8 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         const int d = ct * 16 + (lane & 15);
         if (d >= HD) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = row0 + (lane >> 4) * 4 + r;
-            if (i >= nrows) continue;
-            const int pos = i / a.G, head = kvh * a.G + i % a.G;
-            a.o[b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + d] = f2bf(oacc[c][r]);
-        }
+        for (int r = 0; r < 4; ++r)
+            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
     }
     if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 5);
 }
@@ -400,7 +409,12 @@ __device__ __forceinline__ void fa_comb(float& m, float& l, float m2, float l2) 
     m = M;
 }
 
-template <int HD, int RG, int KSPL>
+// LDS hand-off between the tile loads and the MFMA reads: wait for this wave's own LDS stores,
+// then a raw s_barrier -- __syncthreads()'s release fence would also wait vmcnt(0) and drain the
+// register prefetch of the next PD tiles at every tile
+#define PGMI_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+template <int HD, int RG, int KSPL, int PD>
 __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
     using I = FAInfo<HD>;
     constexpr int KS = I::KS, CT = I::CT, CH = I::CH, KRC = I::KRC, KRS = I::KRS, VS = I::VS;
@@ -439,77 +453,104 @@ __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
     const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
     const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
     const int nt = (a.Lk + TK - 1) / TK;
-    const int nit = (nt + KSPL - 1) / KSPL;  // tiles per split group (every group runs nit barriers)
+    // tiles per split group, padded to whole PD-groups: a tile past the keys is all zeros and
+    // masked (s = -inf, p = 0), so the padded iterations change nothing and the loop body has no
+    // branch around its loads (a branch would make hipcc wait for the whole prefetch)
+    const int nit = ((nt + KSPL - 1) / KSPL + PD - 1) / PD * PD;
 
-    uint4 kr[LCH], vr[LCH];
-    auto gload = [&](int t, bool withv) {
+    // register ring: tile it (it >= 1) of this split group lives in slot (it - 1) % PD from its
+    // issue until it is stored to LDS at iteration it - 1; tile 0 goes straight to LDS buffer 0
+    uint4 kr[PD][LCH], vr[PD][LCH];
+    // every load is issued, unconditionally: rows past the keys (and tiles past the end) read the
+    // last key's row instead -- its scores are masked to -inf and its p is 0, so the duplicate
+    // contributes nothing (V rows are finite data) -- and lanes past the tile's chunks re-read
+    // chunk 0 (not stored).  No select touches a loaded value, so nothing branches around a load.
+    auto gload = [&](int sl, int t, bool withv) {
 #pragma unroll
         for (int i = 0; i < LCH; ++i) {
-            const int e = th + NTH * i;
-            const int key = t * TK + e / CH, ch = e % CH;
-            const bool ok = e < TK * CH && t < nt && key < a.Lk;
-            kr[i] = ldg16_sel(kbase + (long)key * a.k_row_stride + ch * 8, ok, kbase);
-            if (withv) vr[i] = ldg16_sel(vbase + (long)key * a.v_row_stride + ch * 8, ok, vbase);
+            int e = th + NTH * i;
+            if (TK * CH % NTH != 0 && e >= TK * CH) e = 0;
+            int key = t * TK + e / CH;
+            key = key < a.Lk ? key : a.Lk - 1;
+            const int ch = e % CH;
+            kr[sl][i] = ldg16(kbase + (long)key * a.k_row_stride + ch * 8);
+            if (withv) vr[sl][i] = ldg16(vbase + (long)key * a.v_row_stride + ch * 8);
         }
     };
-    auto lstore = [&](int buf, bool withv) {
+    auto lstore = [&](int sl, int buf, bool withv) {
 #pragma unroll
         for (int i = 0; i < LCH; ++i) {
             const int e = th + NTH * i;
             if (e < TK * CH) {
                 const int r = e / CH, ch = e % CH;
-                *reinterpret_cast<uint4*>(Kl + buf * KBUF + r * KRS + ((ch ^ (r & 15)) << 3)) = kr[i];
-                if (withv) *reinterpret_cast<uint4*>(Vl + buf * VBUF + r * VS + ch * 8) = vr[i];
+                *reinterpret_cast<uint4*>(Kl + buf * KBUF + r * KRS + ((ch ^ (r & 15)) << 3)) = kr[sl][i];
+                if (withv) *reinterpret_cast<uint4*>(Vl + buf * VBUF + r * VS + ch * 8) = vr[sl][i];
             }
         }
     };
-    // S^T for the 32 keys of the tile in buffer buf: s[kt][r] = key t*32 + 16kt + 4g + r, query li
+    // S^T for the 32 keys of the tile in buffer buf: s[kt][r] = key t*32 + 16kt + 4g + r, query li.
+    // Even and odd k-steps accumulate in separate registers (two independent MFMA chains per key
+    // half, four in all, instead of one KS-deep dependent chain each), summed once at the end.
     auto scores = [&](int buf, int t, float (&s)[2][4]) {
+        f32x4 acc[2][2];
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-            const int r = kt * 16 + li;
-            const uint16_t* kp = Kl + buf * KBUF + r * KRS;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < 2; ++kt) acc[kt][0] = acc[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                const short8 kf = *reinterpret_cast<const short8*>(kp + (((kk * 4 + g) ^ (r & 15)) << 3));
-                acc = mfma16(kf, qf[kk], acc);
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                const int r = kt * 16 + li;
+                const short8 kf =
+                    *reinterpret_cast<const short8*>(Kl + buf * KBUF + r * KRS + (((kk * 4 + g) ^ (r & 15)) << 3));
+                acc[kt][kk & 1] = mfma16(kf, qf[kk], acc[kt][kk & 1]);
             }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int key = t * TK + kt * 16 + 4 * g + j;
-                s[kt][j] = key < a.Lk ? rbf(rbf(acc[j]) * a.scale) : -INFINITY;
+                const float v = rbf(rbf(acc[kt][0][j] + acc[kt][1][j]) * a.scale);  // computed for every key
+                s[kt][j] = key < a.Lk ? v : -INFINITY;                              // then masked
             }
-        }
+    };
+    // pass prologue: tile 0 -> LDS buffer 0, tiles 1..PD -> the register ring
+    auto prologue = [&](bool withv) {
+        gload(0, ks, withv);
+        lstore(0, 0, withv);
+#pragma unroll
+        for (int q = 0; q < PD; ++q) gload(q, (1 + q) * KSPL + ks, withv);
+        PGMI_LDS_BARRIER();
     };
 
     // ---- pass 1: per-row max and sum of exp
     float m = -INFINITY, l = 0.f;
-    gload(ks, false);
-    lstore(0, false);
-    __syncthreads();
-    for (int it = 0; it < nit; ++it) {
-        const int t = it * KSPL + ks, buf = it & 1;
-        if (it + 1 < nit) gload(t + KSPL, false);
-        float s[2][4];
-        scores(buf, t, s);
-        float tm = -INFINITY;
+    prologue(false);
+    for (int it0 = 0; it0 < nit; it0 += PD) {
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) tm = fmaxf(tm, s[kt][j]);
-        const float mn = fmaxf(m, tm);
-        if (mn != -INFINITY) {
-            float ts = 0.f;
+        for (int q = 0; q < PD; ++q) {
+            const int it = it0 + q;
+            const int t = it * KSPL + ks, buf = it & 1;
+            float s[2][4];
+            scores(buf, t, s);
+            float tm = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) ts += fa_exp(s[kt][j] - mn);
-            l = (m == -INFINITY ? 0.f : l * fa_exp(m - mn)) + ts;
-            m = mn;
+                for (int j = 0; j < 4; ++j) tm = fmaxf(tm, s[kt][j]);
+            const float mn = fmaxf(m, tm);
+            if (mn != -INFINITY) {
+                float ts = 0.f;
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ts += fa_exp(s[kt][j] - mn);
+                l = (m == -INFINITY ? 0.f : l * fa_exp(m - mn)) + ts;
+                m = mn;
+            }
+            lstore(q, buf ^ 1, false);                   // tile it + 1
+            gload(q, (it + 1 + PD) * KSPL + ks, false);  // tile it + 1 + PD into the freed slot
+            PGMI_LDS_BARRIER();
         }
-        if (it + 1 < nit) lstore(buf ^ 1, false);
-        __syncthreads();
     }
     // lanes g = 0..3 of a query, in a fixed order
 #pragma unroll
@@ -541,31 +582,33 @@ __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
     f32x4 oacc[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gload(ks, true);
-    lstore(0, true);
-    __syncthreads();
-    for (int it = 0; it < nit; ++it) {
-        const int t = it * KSPL + ks, buf = it & 1;
-        if (it + 1 < nit) gload(t + KSPL, true);
-        float s[2][4];
-        scores(buf, t, s);
-        short8 pa;
+    prologue(true);
+    for (int it0 = 0; it0 < nit; it0 += PD) {
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
+        for (int q = 0; q < PD; ++q) {
+            const int it = it0 + q;
+            const int t = it * KSPL + ks, buf = it & 1;
+            float s[2][4];
+            scores(buf, t, s);
+            short8 pa;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) pa[kt * 4 + j] = (short)f2bf(fa_exp(s[kt][j] - m) * invl);
-        const uint16_t* vb0 = Vl + buf * VBUF + (4 * g + (li >> 2)) * VS + 4 * (li & 3);
+            for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s4v*)(vb0 + c * 16));
-            const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s4v*)(vb0 + 16 * VS + c * 16));
-            const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            oacc[c] = mfma16(pa, vb, oacc[c]);
+                for (int j = 0; j < 4; ++j) pa[kt * 4 + j] = (short)f2bf(fa_exp(s[kt][j] - m) * invl);
+            const uint16_t* vb0 = Vl + buf * VBUF + (4 * g + (li >> 2)) * VS + 4 * (li & 3);
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s4v*)(vb0 + c * 16));
+                const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s4v*)(vb0 + 16 * VS + c * 16));
+                const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                oacc[c] = mfma16(pa, vb, oacc[c]);
+            }
+            lstore(q, buf ^ 1, true);
+            gload(q, (it + 1 + PD) * KSPL + ks, true);
+            PGMI_LDS_BARRIER();
         }
-        if (it + 1 < nit) lstore(buf ^ 1, true);
-        __syncthreads();
     }
     // split groups 1.. hand their partial O to group 0 through LDS (the tile buffers are free)
     if constexpr (KSPL > 1) {
@@ -585,17 +628,15 @@ __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
                 oacc[c] += *reinterpret_cast<const f32x4*>(ob + ((((q - 1) * RG + rg) * CT + c) * 64 + lane) * 4);
     }
     // C map: d = 16c + li, query row 4g + r of the wave's 16
+    uint16_t* orow[4];
+    attn_out_rows(a, b, kvh, blockIdx.x * (16 * RG) + rg * 16 + 4 * g, nrows, orow);
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int d = c * 16 + li;
         if (d >= HD) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = blockIdx.x * (16 * RG) + rg * 16 + 4 * g + r;
-            if (i >= nrows) continue;
-            const int pos = i / a.G, head = kvh * a.G + i % a.G;
-            a.o[b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + d] = f2bf(oacc[c][r]);
-        }
+        for (int r = 0; r < 4; ++r)
+            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
     }
 }
 
@@ -751,17 +792,15 @@ __global__ void __launch_bounds__(64 * W) k_attn_lds(AttnArgs a) {
             oacc[c] = mfma16(pa, vb, oacc[c]);
         }
     }
+    uint16_t* orow[4];
+    attn_out_rows(a, b, kvh, blockIdx.x * (16 * W) + wave * 16 + 4 * g, nrows, orow);
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int d = c * 16 + li;
         if (d >= HD) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = blockIdx.x * (16 * W) + wave * 16 + 4 * g + r;
-            if (i >= nrows) continue;
-            const int pos = i / a.G, head = kvh * a.G + i % a.G;
-            a.o[b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + d] = f2bf(oacc[c][r]);
-        }
+        for (int r = 0; r < 4; ++r)
+            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
     }
 }
 
@@ -778,19 +817,19 @@ static void launch_attn_lds(hipStream_t s, const AttnArgs& a) {
     hipLaunchKernelGGL((k_attn_lds<HD, W>), grid, dim3(64 * W), lds, s, a);
 }
 
-template <int HD, int RG, int KSPL>
+template <int HD, int RG, int KSPL, int PD = 1>
 static void launch_fa(hipStream_t s, const AttnArgs& a) {
     using I = FAInfo<HD>;
     constexpr size_t lds = (size_t)KSPL * 2 * 32 * (I::KRS + I::VS) * 2 + (size_t)KSPL * RG * 16 * 2 * 4;
     static_assert(lds <= 160 * 1024, "LDS");
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fa<HD, RG, KSPL>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fa<HD, RG, KSPL, PD>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     dim3 grid((a.Lq * a.G + 16 * RG - 1) / (16 * RG), a.n_kv, a.B);
-    hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL>), grid, dim3(64 * RG * KSPL), lds, s, a);
+    hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL, PD>), grid, dim3(64 * RG * KSPL), lds, s, a);
 }
 
 // attention variant override (tuning hook pgmi_tune_attention / env PGMI_ATTN): 0 = the 16-row
@@ -803,17 +842,30 @@ static int g_attn_force = [] {
 
 void attention_force_variant(int v) { g_attn_force = v; }
 
-template <int HD>
-static void launch_fa_variant(hipStream_t s, const AttnArgs& a, int v) {
-    switch (v) {
-        case 41: launch_fa<HD, 4, 1>(s, a); return;
-        case 21: launch_fa<HD, 2, 1>(s, a); return;
-        case 22: launch_fa<HD, 2, 2>(s, a); return;
-        case 44: if constexpr (HD == 72) { launch_fa<HD, 4, 4>(s, a); return; } break;
-        case 24: if constexpr (HD == 72) { launch_fa<HD, 2, 4>(s, a); return; } break;
+// variant = 100 * PD + 10 * RG + KSPL (PD = register prefetch depth in tiles; < 100: PD 1)
+template <int HD, int PD>
+static bool launch_fa_pd(hipStream_t s, const AttnArgs& a, int rk) {
+    switch (rk) {
+        case 41: launch_fa<HD, 4, 1, PD>(s, a); return true;
+        case 42: launch_fa<HD, 4, 2, PD>(s, a); return true;
+        case 21: launch_fa<HD, 2, 1, PD>(s, a); return true;
+        case 22: launch_fa<HD, 2, 2, PD>(s, a); return true;
+        case 44: if constexpr (HD == 72) { launch_fa<HD, 4, 4, PD>(s, a); return true; } break;
+        case 24: if constexpr (HD == 72) { launch_fa<HD, 2, 4, PD>(s, a); return true; } break;
         default: break;
     }
-    launch_fa<HD, 4, 2>(s, a);
+    return false;
+}
+
+template <int HD>
+static void launch_fa_variant(hipStream_t s, const AttnArgs& a, int v) {
+    const int pd = v / 100, rk = v % 100;
+    bool ok = false;
+    if (pd <= 1) ok = launch_fa_pd<HD, 1>(s, a, rk);
+    else if (pd == 2) ok = launch_fa_pd<HD, 2>(s, a, rk);
+    else if (pd == 3) ok = launch_fa_pd<HD, 3>(s, a, rk);
+    else ok = launch_fa_pd<HD, 4>(s, a, rk);
+    if (!ok) launch_fa<HD, 4, 2, 1>(s, a);
 }
 
 static size_t attn_full_lds(int head_dim, int Lk) {
@@ -840,7 +892,7 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         }
         return;
     }
-    if (v >= 91) v = -1;
+    if (v >= 91 && v < 100) v = -1;
     if (v < 0) {
         // measured on MI355X (tools/probes/attn_bench.py, round 1), us per call:
         //   SigLIP 224 (256 rows x 16 heads):  16-row 16.4 | RG2xKSPL4 10.8 | RG4xKSPL2 13.5

@@ -7,7 +7,7 @@ mkdir -p $GRAFT_REPO_ROOT/gpurun_out/ab
 for i in $(seq 1 ${1:-2}); do
   for v in base new; do
     if [ $v = base ]; then export PGMI_LIB_PATH=$B; else unset PGMI_LIB_PATH; fi
-    timeout -k 10 300 python $GRAFT_REPO_ROOT/bench.py --no-448 --no-extra --no-cpu-baseline --prefill-iters 3 \
+    timeout -k 10 300 python $GRAFT_REPO_ROOT/bench.py --no-448 --no-extra --no-api --no-cpu-baseline --prefill-iters 3 \
       > $GRAFT_REPO_ROOT/gpurun_out/ab/b.log 2>&1
     echo "$v $(tail -n 1 $GRAFT_REPO_ROOT/gpurun_out/ab/b.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["prefill_ms"])')"
   done

@@ -14,7 +14,7 @@ from oracle import weights as W  # noqa: E402
 from pgmi import Engine  # noqa: E402
 
 KEYS = ["PGMI_QKV_RPW", "PGMI_QKV_CAP", "PGMI_QKV_UPB", "PGMI_QKV_DEPTH", "PGMI_O_RPW", "PGMI_O_CAP", "PGMI_GU_RPW", "PGMI_GU_CAP", "PGMI_DOWN_RPW",
-        "PGMI_DOWN_CAP", "PGMI_LM_RPW", "PGMI_LM_CAP"]
+        "PGMI_DOWN_CAP", "PGMI_LM_RPW", "PGMI_LM_CAP", "PGMI_GU_DEPTH", "PGMI_DOWN_DEPTH", "PGMI_LM_DEPTH"]
 
 
 def main():

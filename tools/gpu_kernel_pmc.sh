@@ -8,6 +8,10 @@ TAG=${1:-r02}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/kpmc_$TAG
 mkdir -p $OUT
+# heartbeat: a pass can run past gpurun's 180 s silence limit without printing
+( while true; do date +%s >> $OUT/heartbeat; sleep 20; done ) &
+HB=$!
+trap "kill $HB" EXIT
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 16 --warmup 4 --no-cpu-baseline --no-api --prefill-iters 3 --kernel-iters 18 --nokv-tokens 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
@@ -22,7 +26,7 @@ echo fetch done
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
     python3 $R/bench.py $ARGS > $OUT/write.log 2>&1
 echo write done
-python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_stats.csv $OUT/mfma/run_counter_collection.csv \
+python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_trace.csv $OUT/mfma/run_counter_collection.csv \
     $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_pmc.csv > $OUT/summary.txt
 echo done
 python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \

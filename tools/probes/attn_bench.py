@@ -1,6 +1,6 @@
 """Probe: prefill attention kernel time at the PaliGemma shapes (SigLIP / Gemma, 224 / 448 px)
 for every variant of pgmi_tune_attention (0 = 16-row kernel, RK = tiled with R row groups and
-K key splits, -1 = the default choice), plus a rel-L2 check against a torch fp32 attention with
+K key splits, 100 * PD + RK = the same with a register prefetch of PD tiles, -1 = the default choice), plus a rel-L2 check against a torch fp32 attention with
 the reference's rounding points.
     python tools/probes/attn_bench.py [variants...]
 """
@@ -21,9 +21,9 @@ shapes = [("siglip224", 256, 16, 16, 72), ("siglip448", 1024, 16, 16, 72),
 torch.manual_seed(0)
 variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 8, 41, 42, 21, 22, 44, 24, 91, 92, 94]
 for var, (name, L, H, Hkv, d) in [(v, sh) for sh in shapes for v in variants]:
-    if var in (44, 24) and d != 72:
+    if var % 100 in (44, 24) and d != 72:
         continue
-    if (var >= 91 and name != "siglip224") or (var == 8 and name != "gemma224"):
+    if (91 <= var < 100 and name != "siglip224") or (var == 8 and name != "gemma224"):
         continue
     NN.check(eng.lib.pgmi_tune_attention(var))
     scale = d ** -0.5

@@ -24,10 +24,11 @@ constexpr int kAttnDecodeLds = DVH * DVS * 2 + 16 * (DCH + 4) * 4 + 16 * DPS * 2
 
 typedef short s4v_t __attribute__((ext_vector_type(4)));
 
-template <bool C>
-__device__ __forceinline__ short8 frag256(const uint16_t* rowp, bool valid, int kk, int lane) {
+// fragment of a row that is always valid memory (callers clamp the row): an unconditional load,
+// no select on the loaded value (hipcc turns such a select back into a branch around the load)
+__device__ __forceinline__ short8 frag256(const uint16_t* rowp, int kk, int lane) {
     const int k = 32 * kk + 8 * (lane >> 4);
-    return __builtin_bit_cast(short8, ldg16_sel(rowp + k, valid, rowp));
+    return __builtin_bit_cast(short8, ldg16(rowp + k));
 }
 
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
@@ -49,20 +50,22 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
     for (int i = 0; i < DCH * 32 / 256; ++i) {
         const int e = tid + 256 * i, r = e >> 5, c = e & 31;
-        vr[i] = ldg16_sel(vb + (long)(t0 + r) * a.v_row_stride + 8 * c, r < nk, vb);
+        // rows past the cache read the last row instead: their e is 0 (finite data times 0)
+        vr[i] = ldg16(vb + (long)(r < nk ? t0 + r : Lk - 1) * a.v_row_stride + 8 * c);
     }
     const int qi = lane & 15;
     const bool qvalid = qi < a.G;
     const uint16_t* qrow = a.q + b * a.q_b_stride + (kvh * a.G + (qvalid ? qi : 0)) * a.q_head_stride;
     const int key = t0 + wave * 16 + (lane & 15);
-    // rows past the cache are never read: the row is clamped, its fragment zeroed (ldg16_sel)
+    // rows past the cache are never read: the row is clamped (its scores are masked below), and
+    // query lanes past G read head 0 (their score rows are never used)
     const uint16_t* krow = a.k + b * a.k_b_stride + kvh * a.k_head_stride + (long)(key < Lk ? key : 0) * a.k_row_stride;
     short8 qf[8], kf[8];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256<false>(krow, key < Lk, kk, lane);
+    for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256(krow, kk, lane);
 
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256<false>(qrow, qvalid, kk, lane);
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256(qrow, kk, lane);
 
     // ---- scores (MFMA): wave w -> keys t0 + 16w + (lane & 15)
     {

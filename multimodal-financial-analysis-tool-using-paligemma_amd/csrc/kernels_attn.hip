@@ -31,10 +31,16 @@ struct HDInfo {
 };
 
 // load the 16-row A (or B) fragment: lane -> row (lane&15), k = 32*kk + 8*(lane>>4)
+// The row must be valid memory: callers clamp rows past the end (their scores are masked or their
+// outputs never stored), so the load is unconditional -- a select on a loaded value is turned back
+// into a branch around the load by hipcc.  Only head dims that are not a multiple of 32 zero the
+// k range past HD (HD 72: the last 32-deep step).
 template <int HD>
-__device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool valid, int kk, int lane) {
+__device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool /*row valid: clamped by the caller*/,
+                                            int kk, int lane) {
     const int k = 32 * kk + 8 * (lane >> 4);
-    return __builtin_bit_cast(short8, ldg16_sel(rowp + k, valid && k < HD, rowp));
+    if constexpr (HD % 32 == 0) return __builtin_bit_cast(short8, ldg16(rowp + k));
+    else return __builtin_bit_cast(short8, ldg16_sel(rowp + k, k < HD, rowp));
 }
 
 typedef s4v_t s4v;
@@ -144,7 +150,8 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
             const int e = tid + 256 * i;
             const int tt = e / I::CH, ch = e % I::CH;
             const int key = t0 + tt;
-            vr[i] = ldg16_sel(vbase + (long)key * a.v_row_stride + ch * 8, e < CHK * I::CH && key < a.Lk, vbase);
+            vr[i] = (e < CHK * I::CH) ? ldg16(vbase + (long)(key < a.Lk ? key : a.Lk - 1) * a.v_row_stride + ch * 8)
+                                      : make_uint4(0, 0, 0, 0);  // rows past the keys: p = 0
         }
     };
     auto vstore = [&](int buf) {
@@ -215,6 +222,7 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     constexpr int VS = HDP + 16;
     constexpr int CHK = 32;
     constexpr int VPT = (CHK * I::CH + 255) / 256;
+    static_assert(CHK * I::CH % 256 == 0, "every thread loads whole V chunks (no tail lanes)");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int LkP = (a.Lk + 31) & ~31;
     uint16_t* S = reinterpret_cast<uint16_t*>(smem_raw);  // [16][LkP] bf16 P
@@ -254,7 +262,7 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         for (int i = 0; i < VPT; ++i) {
             const int e = tid + 256 * i;
             const int key = c * CHK + e / I::CH, ch = e % I::CH;
-            vr[c][i] = ldg16_sel(vbase + (long)key * a.v_row_stride + ch * 8, e < CHK * I::CH && key < a.Lk, vbase);
+            vr[c][i] = ldg16(vbase + (long)(key < a.Lk ? key : a.Lk - 1) * a.v_row_stride + ch * 8);  // p = 0 past Lk
         }
     if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 1);
 

@@ -302,6 +302,10 @@ class GemmaForCausalLM(nn.Module):
     def tie_weights(self):
         self.lm_head.weight = self.model.embed_tokens.weight
 
+    def pgmi_rebind(self):
+        """Forget the engine binding (after replacing Parameter objects; pgmi/binding.py)."""
+        _binding.unbind(self)
+
     def _pgmi_engine(self):
         owner = _binding.owner_of(self)
         if owner is not None:
@@ -394,6 +398,11 @@ class PaliGemmaForConditionalGeneration(nn.Module):
 
     def prepare_inputs_for_generation(self, input_ids=None, **kwargs):
         return {"input_ids": input_ids, **kwargs}
+
+    def pgmi_rebind(self):
+        """Forget the engine binding (after replacing Parameter objects): the next forward copies
+        the current parameters into a new weight slab (pgmi/binding.py)."""
+        _binding.unbind(self)
 
     def _pgmi_engine(self):
         _check_tied(self.language_model)

@@ -20,14 +20,19 @@ echo trace done
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE \
     --output-format csv -d $OUT/mfma -o run -- python3 $R/bench.py $ARGS > $OUT/mfma.log 2>&1
 echo mfma done
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-    python3 $R/bench.py $ARGS > $OUT/fetch.log 2>&1
+# FETCH_SIZE / WRITE_SIZE over the short probe (prefill + eager decode, B = 1 and 8): a TCC pass
+# over bench.py's every-leg run does not finish
+P="python3 $R/tools/probes/pmc_probe.py 3"
+timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/ptrace -o run -- $P > $OUT/ptrace.log 2>&1
+echo probe trace done
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $P > $OUT/fetch.log 2>&1
 echo fetch done
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-    python3 $R/bench.py $ARGS > $OUT/write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $P > $OUT/write.log 2>&1
 echo write done
 python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_trace.csv $OUT/mfma/run_counter_collection.csv \
-    $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_pmc.csv > $OUT/summary.txt
+    - - $OUT/kernel_pmc_bench.csv > $OUT/summary.txt
+python3 $R/tools/kernel_pmc.py $OUT/ptrace/run_kernel_trace.csv - \
+    $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_hbm_probe.csv >> $OUT/summary.txt
 echo done
 python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     "k_gemv<1, 4, 1, 2, 1, true, 1>" gateup $OUT/pmc_traffic.json >> $OUT/summary.txt

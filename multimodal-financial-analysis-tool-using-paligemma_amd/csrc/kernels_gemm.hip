@@ -40,6 +40,66 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float
     }
 }
 
+// Epilogue of a wave's TM x TN MFMA tiles (C map of 16x16x32: column nb + 16 j + (lane & 15), rows
+// mb + 16 i + 4 (lane >> 4) + r).  Every operand the epilogue reads -- bias per column, residual /
+// position rows per element -- is loaded first from a clamped (always valid) address, and only the
+// stores sit under the bounds guard: a guarded load makes hipcc branch around it and wait
+// vmcnt(0) per element (one dependent round trip per output).
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb, int nb, int lane,
+                                         const f32x4 (&acc)[TM][TN], const f32x4 (&acc2)[TM][TN]) {
+    constexpr bool HB = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_POS;
+    constexpr bool HR = EPI == EPI_BIAS_RES || EPI == EPI_RES;
+    constexpr bool HP = EPI == EPI_BIAS_POS;
+    int ncl[TN];
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = nb + j * 16 + (lane & 15);
+        ncl[j] = n < N ? n : N - 1;
+        if constexpr (HB) bv[j] = bf2f(ea.bias[ncl[j]]);
+        else bv[j] = 0.f;
+    }
+    float xv[TM][TN][4];
+    if constexpr (HR || HP) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = mb + i * 16 + (lane >> 4) * 4 + r;
+                m = m < M ? m : M - 1;
+                const uint16_t* row;
+                if constexpr (HR) row = ea.res + (long)m * ea.ldr;
+                else row = ea.pos + (long)(m % ea.npos) * ea.ldo;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) xv[i][j][r] = bf2f(row[ncl[j]]);
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = nb + j * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+                const float a = acc[i][j][r];
+                float o = 0.f;
+                if constexpr (EPI == EPI_STORE) o = a;
+                else if constexpr (EPI == EPI_BIAS) o = a + bv[j];
+                else if constexpr (EPI == EPI_BIAS_GELU) o = gelu_tanh(rbf(a + bv[j]));
+                else if constexpr (EPI == EPI_BIAS_RES) o = rbf(a + bv[j]) + xv[i][j][r];
+                else if constexpr (EPI == EPI_RES) o = rbf(a) + xv[i][j][r];
+                else if constexpr (EPI == EPI_BIAS_POS) o = rbf(a + bv[j]) + xv[i][j][r];
+                else if constexpr (EPI == EPI_GEGLU) o = rbf(gelu_tanh(rbf(a))) * rbf(acc2[i][j][r]);
+                if (m < M && n < N) {
+                    if constexpr (EPI == EPI_F32) ea.out_f32[(long)m * ea.ldo + n] = rbf(a);
+                    else ea.out[(long)m * ea.ldo + n] = f2bf(o);
+                }
+            }
+        }
+}
+
 // SPLIT: write raw fp32 partials to ws[z][M][N] (z = blockIdx.z) instead of the epilogue.
 // Wave grid WGM x WGN; each wave owns TM x TN 16x16 MFMA tiles, so BM = WGM*TM*16 and
 // BN = WGN*TN*16.  Small-M prefill GEMMs (M = 256 vision rows, 288 text rows) use one
@@ -383,23 +443,21 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #undef PGMI_SB
 
     // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                if (m < M && n < N) {
-                    if constexpr (SPLIT) {
-                        ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
-                    } else {
-                        epi_store<EPI>(ea, m, n, acc[0][i][j][r], NB == 2 ? acc[NB - 1][i][j][r] : 0.f);
-                    }
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
+                    if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
-        }
+    } else {
+        epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
+    }
 }
 
 // ---------------------------------------------------------------- warp-specialised panel GEMM
@@ -543,23 +601,21 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
         }
         slot = slot + 1 == ST ? 0 : slot + 1;
     }
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                if (m < M && n < N) {
-                    if constexpr (SPLIT) {
-                        ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
-                    } else {
-                        epi_store<EPI>(ea, m, n, acc[0][i][j][r], NB == 2 ? acc[NB - 1][i][j][r] : 0.f);
-                    }
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
+                    if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
-        }
+    } else {
+        epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
+    }
 }
 
 // Tile configurations (wave grid, per-wave MFMA tiles).  BM = WGM*TM*16, BN = WGN*TN*16.
@@ -875,6 +931,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
     if (p.split > 1 && (size_t)p.split * M * N * sizeof(float) > ws_bytes) p.split = 1;
     if (p.split > 1 && N % 4 != 0) p.split = 1;  // the split-K epilogue works on 4 outputs per thread
     const long up_off = (long)up_offset_rows * ldw;
+    if (defer && p.split > 8) p.split = 8;  // the consumers (splitk_res_norm, rope_kv) reduce at most 8 slabs
     if (defer && p.split > 1) {
         // partial slabs only: the consumer kernel (splitk_res_norm / rope_kv_append) reduces them
         switch (p.cfg) {

@@ -7,6 +7,8 @@
 //   rope_kv_append rotary + KVCache.update modeling_gemma.py:143-199,259, :10-36
 //   patchify       Conv2d(k=s=14) as im2col (+ pixel cast to bf16)  modeling_siglip.py:45-51,67; modeling_gemma.py:570
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 #include "launch.h"
@@ -248,11 +250,31 @@ __global__ void k_rope_kv(const uint16_t* __restrict__ qkv, const float* __restr
             return bf2f(qkv[r * ncol + c]);
         }
     };
-    // pairs (d, d+128) of every rotated head: nh + nkv heads x 128 pairs
-    for (int u = threadIdx.x; u < (nh + nkv) * 128; u += blockDim.x) {
+    // pairs (d, d+128) of every rotated head: nh + nkv heads x 128 pairs.  A thread's pairs (at most
+    // kRopeIt; rows past the end re-read the last pair and are not stored), their cos/sin and its V
+    // column are all loaded before the first is used: one memory round trip per row
+    constexpr int kRopeIt = 5;  // ceil((8 + 1) * 128 / 256) at PaliGemma's 8 q heads + 1 kv head
+    const int npair = (nh + nkv) * 128;
+    float av[kRopeIt], bv[kRopeIt], cv[kRopeIt], sv[kRopeIt];
+#pragma unroll
+    for (int i = 0; i < kRopeIt; ++i) {
+        int u = threadIdx.x + i * blockDim.x;
+        u = u < npair ? u : npair - 1;
         const int hh = u >> 7, d = u & 127;
-        const float a = val(hh * 256 + d), bb = val(hh * 256 + d + 128);
-        const float c = bf2f(cosT[p * 128 + d]), sn = bf2f(sinT[p * 128 + d]);
+        av[i] = val(hh * 256 + d);
+        bv[i] = val(hh * 256 + d + 128);
+        cv[i] = bf2f(cosT[p * 128 + d]);
+        sv[i] = bf2f(sinT[p * 128 + d]);
+    }
+    const int vcols = nkv * 256;
+    const int vu = (int)threadIdx.x < vcols ? (int)threadIdx.x : vcols - 1;
+    const float vval = val((nh + nkv) * 256 + vu);
+#pragma unroll
+    for (int i = 0; i < kRopeIt; ++i) {
+        const int u = threadIdx.x + i * blockDim.x;
+        if (u >= npair) break;
+        const int hh = u >> 7, d = u & 127;
+        const float a = av[i], bb = bv[i], c = cv[i], sn = sv[i];
         const uint16_t oa = f2bf(rbf(a * c) + rbf(-bb * sn));
         const uint16_t ob = f2bf(rbf(bb * c) + rbf(a * sn));
         if (hh < nh) {
@@ -265,9 +287,25 @@ __global__ void k_rope_kv(const uint16_t* __restrict__ qkv, const float* __restr
             dst[d + 128] = ob;
         }
     }
-    for (int u = threadIdx.x; u < nkv * 256; u += blockDim.x) {
-        vc[b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + u] = f2bf(val((nh + nkv) * 256 + u));
+    if ((int)threadIdx.x < vcols) vc[b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + threadIdx.x] = f2bf(vval);
+    // (shapes beyond the unrolled coverage: the remaining pairs and V columns, plain loop)
+    for (int u = threadIdx.x + kRopeIt * blockDim.x; u < npair; u += blockDim.x) {
+        const int hh = u >> 7, d = u & 127;
+        const float a = val(hh * 256 + d), bb = val(hh * 256 + d + 128);
+        const float c = bf2f(cosT[p * 128 + d]), sn = bf2f(sinT[p * 128 + d]);
+        const uint16_t oa = f2bf(rbf(a * c) + rbf(-bb * sn));
+        const uint16_t ob = f2bf(rbf(bb * c) + rbf(a * sn));
+        if (hh < nh) {
+            q_out[r * (nh * 256) + hh * 256 + d] = oa;
+            q_out[r * (nh * 256) + hh * 256 + d + 128] = ob;
+        } else {
+            uint16_t* dst = kc + b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + (hh - nh) * 256;
+            dst[d] = oa;
+            dst[d + 128] = ob;
+        }
     }
+    for (int u = threadIdx.x + blockDim.x; u < vcols; u += blockDim.x)
+        vc[b * kv_b_stride + (long)(kv_start + l) * (nkv * 256) + u] = f2bf(val((nh + nkv) * 256 + u));
 }
 
 void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int split, int B, int L, int nh, int nkv,
@@ -283,7 +321,11 @@ void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int spl
 }
 
 // ---------------------------------------------------------------- split-K reduce + residual + norm
-// Row per workgroup, 256 threads x 8 columns x 2 chunks (D <= 4096).
+// Row per workgroup, 256 threads x 8 columns x 2 chunks (D <= 4096).  Every global read of the
+// row -- residual h, the split-K partial slabs (up to kMaxSplit, clamped to the live ones and
+// weighted 0 past `split`), bias, and the norm's weight / bias -- is issued before the first is
+// consumed: one memory round trip per row instead of one per slab plus one after the reductions.
+constexpr int kMaxSplit = 8;
 template <bool LN>
 __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict__ ws, int split, long slab,
                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ h,
@@ -292,6 +334,7 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
     __shared__ float red[4];
     const long row = blockIdx.x;
     float v[16];
+    uint4 wv[2], bnv[2];
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
         const int c = (threadIdx.x + it * 256) * 8;
@@ -300,19 +343,28 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
             for (int j = 0; j < 8; ++j) v[it * 8 + j] = 0.f;
             continue;
         }
-        uint4 hv = ldg16(h + row * D + c);
+        const uint4 hv = ldg16(h + row * D + c);
+        wv[it] = ldg16(w + c);
+        if constexpr (LN) bnv[it] = ldg16(b + c);
         const uint16_t* he = reinterpret_cast<const uint16_t*>(&hv);
         if (split > 1) {
+            const uint4 bv = ldg16(bias ? bias + c : h + row * D + c);  // (h: any valid address, unused)
+            f32x4 p0[kMaxSplit], p1[kMaxSplit];
+#pragma unroll
+            for (int z = 0; z < kMaxSplit; ++z) {
+                const long zo = (long)(z < split ? z : 0) * slab + row * D + c;
+                p0[z] = *reinterpret_cast<const f32x4*>(ws + zo);
+                p1[z] = *reinterpret_cast<const f32x4*>(ws + zo + 4);
+            }
             float a[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a[j] = 0.f;
-            for (int z = 0; z < split; ++z) {
-                const f32x4 p0 = *reinterpret_cast<const f32x4*>(ws + z * slab + row * D + c);
-                const f32x4 p1 = *reinterpret_cast<const f32x4*>(ws + z * slab + row * D + c + 4);
+            for (int j = 0; j < 4; ++j) { a[j] = p0[0][j]; a[4 + j] = p1[0][j]; }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) { a[j] += p0[j]; a[4 + j] += p1[j]; }
+            for (int z = 1; z < kMaxSplit; ++z) {
+                const float m = z < split ? 1.f : 0.f;  // slabs in a fixed order; past `split`: + 0
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { a[j] += p0[z][j] * m; a[4 + j] += p1[z][j] * m; }
             }
-            uint4 bv = bias ? ldg16(bias + c) : make_uint4(0, 0, 0, 0);
             const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
             u16x8 o;
 #pragma unroll
@@ -350,12 +402,10 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
     for (int it = 0; it < 2; ++it) {
         const int c = (threadIdx.x + it * 256) * 8;
         if (c >= D) continue;
-        uint4 wv = ldg16(w + c);
-        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv[it]);
         u16x8 o;
         if constexpr (LN) {
-            uint4 bv = ldg16(b + c);
-            const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
+            const uint16_t* be = reinterpret_cast<const uint16_t*>(&bnv[it]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o.v[j] = f2bf((v[it * 8 + j] - mu) * r * bf2f(we[j]) + bf2f(be[j]));
         } else {
@@ -369,6 +419,10 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
 void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                      const uint16_t* b, float eps, uint16_t* out, int rows, int D) {
     const long slab = (long)rows * D;
+    if (split > kMaxSplit) {
+        fprintf(stderr, "pgmi: splitk_res_norm: split %d > %d\n", split, kMaxSplit);
+        std::abort();
+    }
     if (b)
         hipLaunchKernelGGL(k_splitk_res_norm<true>, dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, w, b, eps,
                            out, D);

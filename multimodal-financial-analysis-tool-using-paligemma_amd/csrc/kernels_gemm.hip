@@ -42,26 +42,31 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float
 
 // Epilogue of a wave's TM x TN MFMA tiles (C map of 16x16x32: column nb + 16 j + (lane & 15), rows
 // mb + 16 i + 4 (lane >> 4) + r).  Every operand the epilogue reads -- bias per column, residual /
-// position rows per element -- is loaded first from a clamped (always valid) address, and only the
-// stores sit under the bounds guard: a guarded load makes hipcc branch around it and wait
-// vmcnt(0) per element (one dependent round trip per output).
+// position rows per element -- is loaded first from a clamped (always valid) address (epi_load),
+// and only the stores sit under the bounds guard (epi_apply): a guarded load makes hipcc branch
+// around it and wait vmcnt(0) per element (one dependent round trip per output).  In a kernel
+// whose waves also issue LDS-DMA, hipcc waits vmcnt(0) after every ordinary load anyway, so
+// k_gemm_p issues epi_load before its ring starts (the values wait in registers).
 template <int EPI, int TM, int TN>
-__device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb, int nb, int lane,
-                                         const f32x4 (&acc)[TM][TN], const f32x4 (&acc2)[TM][TN]) {
-    constexpr bool HB = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_POS;
-    constexpr bool HR = EPI == EPI_BIAS_RES || EPI == EPI_RES;
-    constexpr bool HP = EPI == EPI_BIAS_POS;
+struct EpiOps {
+    static constexpr bool HB = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_POS;
+    static constexpr bool HX = EPI == EPI_BIAS_RES || EPI == EPI_RES || EPI == EPI_BIAS_POS;
+    float bv[HB ? TN : 1];
+    float xv[HX ? TM : 1][HX ? TN : 1][4];
+};
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void epi_load(const EpiArgs& ea, int M, int N, int mb, int nb, int lane,
+                                         EpiOps<EPI, TM, TN>& e) {
+    using E = EpiOps<EPI, TM, TN>;
     int ncl[TN];
-    float bv[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = nb + j * 16 + (lane & 15);
         ncl[j] = n < N ? n : N - 1;
-        if constexpr (HB) bv[j] = bf2f(ea.bias[ncl[j]]);
-        else bv[j] = 0.f;
+        if constexpr (E::HB) e.bv[j] = bf2f(ea.bias[ncl[j]]);
     }
-    float xv[TM][TN][4];
-    if constexpr (HR || HP) {
+    if constexpr (E::HX) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -69,11 +74,33 @@ __device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb
                 int m = mb + i * 16 + (lane >> 4) * 4 + r;
                 m = m < M ? m : M - 1;
                 const uint16_t* row;
-                if constexpr (HR) row = ea.res + (long)m * ea.ldr;
-                else row = ea.pos + (long)(m % ea.npos) * ea.ldo;
+                if constexpr (EPI == EPI_BIAS_POS) row = ea.pos + (long)(m % ea.npos) * ea.ldo;
+                else row = ea.res + (long)m * ea.ldr;
 #pragma unroll
-                for (int j = 0; j < TN; ++j) xv[i][j][r] = bf2f(row[ncl[j]]);
+                for (int j = 0; j < TN; ++j) e.xv[i][j][r] = bf2f(row[ncl[j]]);
             }
+    }
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void epi_apply(const EpiArgs& ea, int M, int N, int mb, int nb, int lane,
+                                          EpiOps<EPI, TM, TN>& e, const f32x4 (&acc)[TM][TN],
+                                          const f32x4 (&acc2)[TM][TN]) {
+    // every operand passes through an empty asm before the first store: the loads are waited for
+    // once, here, and the stores below are not mistaken for loads still in flight (on gfx9 vmcnt
+    // counts stores too, so a wait placed between two stores would also wait for the first)
+    using E = EpiOps<EPI, TM, TN>;
+    if constexpr (E::HB) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(e.bv[j]));
+    }
+    if constexpr (E::HX) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(e.xv[i][j][r]));
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -86,11 +113,11 @@ __device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb
                 const float a = acc[i][j][r];
                 float o = 0.f;
                 if constexpr (EPI == EPI_STORE) o = a;
-                else if constexpr (EPI == EPI_BIAS) o = a + bv[j];
-                else if constexpr (EPI == EPI_BIAS_GELU) o = gelu_tanh(rbf(a + bv[j]));
-                else if constexpr (EPI == EPI_BIAS_RES) o = rbf(a + bv[j]) + xv[i][j][r];
-                else if constexpr (EPI == EPI_RES) o = rbf(a) + xv[i][j][r];
-                else if constexpr (EPI == EPI_BIAS_POS) o = rbf(a + bv[j]) + xv[i][j][r];
+                else if constexpr (EPI == EPI_BIAS) o = a + e.bv[j];
+                else if constexpr (EPI == EPI_BIAS_GELU) o = gelu_tanh(rbf(a + e.bv[j]));
+                else if constexpr (EPI == EPI_BIAS_RES) o = rbf(a + e.bv[j]) + e.xv[i][j][r];
+                else if constexpr (EPI == EPI_RES) o = rbf(a) + e.xv[i][j][r];
+                else if constexpr (EPI == EPI_BIAS_POS) o = rbf(a + e.bv[j]) + e.xv[i][j][r];
                 else if constexpr (EPI == EPI_GEGLU) o = rbf(gelu_tanh(rbf(a))) * rbf(acc2[i][j][r]);
                 if (m < M && n < N) {
                     if constexpr (EPI == EPI_F32) ea.out_f32[(long)m * ea.ldo + n] = rbf(a);
@@ -98,6 +125,14 @@ __device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb
                 }
             }
         }
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb, int nb, int lane,
+                                         const f32x4 (&acc)[TM][TN], const f32x4 (&acc2)[TM][TN]) {
+    EpiOps<EPI, TM, TN> e;
+    epi_load<EPI, TM, TN>(ea, M, N, mb, nb, lane, e);
+    epi_apply<EPI, TM, TN>(ea, M, N, mb, nb, lane, e, acc, acc2);
 }
 
 // SPLIT: write raw fp32 partials to ws[z][M][N] (z = blockIdx.z) instead of the epilogue.
@@ -399,6 +434,11 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
                 mfma16(FA[i_], FB[b_][j_], acc[b_][i_][j_]);                                                \
     } while (0)
 
+    // epilogue operands first (see epi_load): held in registers through the k loop
+    const int epi_mb = m0 + wm * TM * 16, epi_nb = n0 + wn * TN * 16;
+    EpiOps<EPI, TM, TN> epi_ops;
+    if constexpr (!SPLIT) epi_load<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops);
+
     // ring: tiles t+1 .. t+ST-1 in flight or landed while tile t is multiplied.  Per tile:
     //   read kk=1 fragments | MFMAs kk=0 | retire tile t+1, barrier, refill the slot tile t
     //   lived in with tile t+ST | read tile t+1's kk=0 fragments | MFMAs kk=1
@@ -456,7 +496,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
                 }
             }
     } else {
-        epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
+        epi_apply<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops, acc[0], acc[NB - 1]);
     }
 }
 

@@ -113,8 +113,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     // clamped) so no branch splits the loads; they go out BEFORE the
     // weight stream, so the norm is computed while the weights are in flight (vmcnt is in
     // order: a load issued after the weights could only be consumed after all of them landed)
+    // the residual modes never normalise their input (down_proj / o_proj): no norm registers
+    constexpr bool NORM = MODE != GV_RES && MODE != GV_ORES;
     uint4 xr[XREG ? B : 1][XREG ? KCW : 1];
-    uint4 nw[XREG ? KCW : 1];
+    uint4 nw[XREG && NORM ? KCW : 1];
     auto load_x = [&]() {
         if constexpr (XREG && MODE != GV_ORES) {
 #pragma unroll
@@ -123,7 +125,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
                 for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<false>(a.x + (long)bq * K + kofs + 512 * c);
             }
-            if (a.norm_w) {
+            if (NORM && a.norm_w) {
 #pragma unroll
                 for (int c = 0; c < KCW; ++c) nw[c] = ldg16(a.norm_w + kofs + 512 * c);
             }
@@ -214,7 +216,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             if (b >= a.nb)
 #pragma unroll
                 for (int c = 0; c < KCW; ++c) xr[b][c] = make_uint4(0, 0, 0, 0);
-        if (a.norm_w) {  // WK == 1: the wave holds the whole row
+        if (NORM && a.norm_w) {  // WK == 1: the wave holds the whole row
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 float ss = 0.f;

@@ -79,7 +79,10 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
             if (nb <= 1) {
                 const int cap = tune_variant("PGMI_DOWN_CAP", 512);
                 const int rpw = tune_variant("PGMI_DOWN_RPW", 1);
+                const int wk = tune_variant("PGMI_DOWN_WK", 4);
                 if (tune_variant("PGMI_DOWN_DEPTH", 1) == 2) launch_gemv<1, 32, 1, GV_RES, 4, 2>(s, c, cap);
+                else if (wk == 2) launch_gemv<1, 32, 1, GV_RES, 2>(s, c, cap);
+                else if (wk == 1) launch_gemv<1, 32, 1, GV_RES, 1>(s, c, cap);
                 else if (rpw == 1) launch_gemv<1, 32, 1, GV_RES, 4>(s, c, cap);
                 else launch_gemv<1, 32, 2, GV_RES, 4>(s, c, cap);
             }

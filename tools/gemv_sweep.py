@@ -30,16 +30,32 @@ def main():
     e = Engine(W.full_config(224), max_batch=1, max_seq=320, max_kv=512)
     e.fill_synthetic(1234, W.init_policy)
     e.prepare()
-    for rpw in (1, 2):
-        for cap in (256, 384, 512, 768, 1024):
+    for rpw in (1,):
+        for cap in (1024,):
             os.environ["PGMI_GU_RPW"], os.environ["PGMI_GU_CAP"] = str(rpw), str(cap)
             t = timeit(e, 2)
             print(f"gate/up rpw {rpw} cap {cap:4d}: {t:6.2f} us  {134217728 / t / 1e3:6.0f} GB/s", flush=True)
-    for rpw in (1, 2):
-        for cap in (128, 256, 384, 512, 768):
-            os.environ["PGMI_DOWN_RPW"], os.environ["PGMI_DOWN_CAP"] = str(rpw), str(cap)
+    os.environ.pop("PGMI_GU_RPW"); os.environ.pop("PGMI_GU_CAP")
+    for depth in (1, 2):
+        for rpw in ((1, 2) if depth == 1 else (1,)):
+            for cap in (256, 512, 768, 1024):
+                os.environ["PGMI_DOWN_DEPTH"] = str(depth)
+                os.environ["PGMI_DOWN_RPW"], os.environ["PGMI_DOWN_CAP"] = str(rpw), str(cap)
+                t = timeit(e, 3)
+                print(f"down depth {depth} rpw {rpw} cap {cap:4d}: {t:6.2f} us  {67108864 / t / 1e3:6.0f} GB/s", flush=True)
+    for k in ("PGMI_DOWN_DEPTH", "PGMI_DOWN_RPW", "PGMI_DOWN_CAP"):
+        os.environ.pop(k)
+    for wk in (2, 1):
+        for cap in (256, 512, 1024, 2048):
+            os.environ["PGMI_DOWN_WK"], os.environ["PGMI_DOWN_CAP"] = str(wk), str(cap)
             t = timeit(e, 3)
-            print(f"down rpw {rpw} cap {cap:4d}: {t:6.2f} us  {67108864 / t / 1e3:6.0f} GB/s", flush=True)
+            print(f"down wk {wk} cap {cap:4d}: {t:6.2f} us  {67108864 / t / 1e3:6.0f} GB/s", flush=True)
+    os.environ.pop("PGMI_DOWN_WK"); os.environ.pop("PGMI_DOWN_CAP")
+    for rpw in (2, 4):
+        for cap in (768, 1024, 2048):
+            os.environ["PGMI_LM_RPW"], os.environ["PGMI_LM_CAP"] = str(rpw), str(cap)
+            t = timeit(e, 4, iters=20)
+            print(f"lm_head rpw {rpw} cap {cap:4d}: {t:7.2f} us  {1053556736 / t / 1e3:6.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -16,6 +16,8 @@ from pgmi import Engine  # noqa: E402
 from pgmi import _native as NN  # noqa: E402
 
 eng = Engine(W.small_config(vision_layers=1, text_layers=1, vocab=1024), max_batch=1, max_seq=64, max_kv=64)
+eng.fill_synthetic(1, W.init_policy)
+eng.prepare()
 shapes = [("siglip224", 256, 16, 16, 72), ("siglip448", 1024, 16, 16, 72),
           ("gemma224", 288, 8, 1, 256), ("gemma448", 1056, 8, 1, 256)]
 torch.manual_seed(0)

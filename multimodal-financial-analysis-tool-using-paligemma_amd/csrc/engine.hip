@@ -824,12 +824,19 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const uint16_t* E = W(x, "language_model.model.embed_tokens.weight");
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
-    embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    // B <= 2: the embedding row is read by layer 0's q|k|v GEMV itself (one launch fewer per step)
+    static const bool fold_env = [] {
+        const char* e = std::getenv("PGMI_EMBED_FOLD");
+        return !e || std::atoi(e) != 0;
+    }();
+    const bool fold = fold_env && gemv_qkv_folds_embed(B) && c.t_layers > 0;
+    const EmbedFold emb{ids, E, normalizer, c.pad_token_id, x->dH};
+    if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
         gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
-                 x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws);
+                 x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws, (fold && i == 0) ? &emb : nullptr);
         AttnArgs a{};
         a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;

@@ -58,6 +58,14 @@ struct GemvArgs {
     int max_chunks;
     int G;
     uint16_t* o_out;
+    // QKV of decode layer 0 (EMB kernels): x is the token's embedding row, bf16(E[id] * normalizer)
+    // (modeling_gemma.py:565,368; a pad id gives a zero row), read here instead of from a separate
+    // embedding launch; workgroup 0 also stores it to emb_out (the layer's residual h)
+    const int64_t* ids;
+    const uint16_t* E;
+    float normalizer;
+    int64_t pad_id;
+    uint16_t* emb_out;
 };
 
 // WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their
@@ -65,8 +73,9 @@ struct GemvArgs {
 // XREG: the activation lives in registers (lane's own K chunks), the RMSNorm is computed
 // per wave (WK == 1: every wave holds the whole row), no LDS staging / barrier; used when
 // B * K/(512*WK) chunks fit in 32 VGPRs.  Otherwise the activation is staged in LDS.
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH = 1>
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH = 1, bool EMB = false>
 __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, const int nblk, uint16_t* xs) {
+    static_assert(!EMB || (MODE == GV_QKV && XREG && WK == 1), "embedding fold: register-held q|k|v input only");
     constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
     constexpr int KCW = KCH / WK;  // chunks per wave
     constexpr int NL = RPW * NR * KCW;
@@ -122,8 +131,15 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
             for (int b = 0; b < B; ++b) {
                 const int bq = b < a.nb ? b : a.nb - 1;
+                const uint16_t* xrow;
+                if constexpr (EMB) {
+                    const int64_t id = a.ids[bq];  // wave-uniform: a scalar load
+                    xrow = a.E + (id == a.pad_id ? 0 : id) * (long)K;
+                } else {
+                    xrow = a.x + (long)bq * K;
+                }
 #pragma unroll
-                for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<false>(a.x + (long)bq * K + kofs + 512 * c);
+                for (int c = 0; c < KCW; ++c) xr[b][c] = ldx16<false>(xrow + kofs + 512 * c);
             }
             if (NORM && a.norm_w) {
 #pragma unroll
@@ -216,6 +232,23 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             if (b >= a.nb)
 #pragma unroll
                 for (int c = 0; c < KCW; ++c) xr[b][c] = make_uint4(0, 0, 0, 0);
+        if constexpr (EMB) {
+            // x = bf16(E[id] * normalizer) (a pad id: zeros), the residual stream of layer 0
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const bool pad = a.ids[b < a.nb ? b : a.nb - 1] == a.pad_id;
+#pragma unroll
+                for (int c = 0; c < KCW; ++c) {
+                    const uint16_t* e = reinterpret_cast<const uint16_t*>(&xr[b][c]);
+                    u16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o.v[j] = pad ? (uint16_t)0 : f2bf(bf2f(e[j]) * a.normalizer);
+                    xr[b][c] = *reinterpret_cast<const uint4*>(&o);
+                    if (blk == 0 && wave == 0 && b < a.nb)
+                        *reinterpret_cast<uint4*>(a.emb_out + (long)b * K + kofs + 512 * c) = xr[b][c];
+                }
+            }
+        }
         if (NORM && a.norm_w) {  // WK == 1: the wave holds the whole row
 #pragma unroll
             for (int b = 0; b < B; ++b) {
@@ -522,10 +555,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     }
 }
 
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH>
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH, bool EMB = false>
 __global__ void __launch_bounds__(256) k_gemv(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [B][K]
-    gemv_block<B, KCH, RPW, MODE, WK, XREG, DEPTH>(a, blockIdx.x, gridDim.x, xs);
+    gemv_block<B, KCH, RPW, MODE, WK, XREG, DEPTH, EMB>(a, blockIdx.x, gridDim.x, xs);
 }
 
 }  // namespace pgmi

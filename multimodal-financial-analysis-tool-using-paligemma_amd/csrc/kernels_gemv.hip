@@ -19,30 +19,39 @@ static int tune_variant(const char* env, int dflt) {
     return v ? std::atoi(v) : dflt;
 }
 
-template <int B, int KCH, int RPW, int MODE, int WK = 1, int DEPTH = 1>
+template <int B, int KCH, int RPW, int MODE, int WK = 1, int DEPTH = 1, bool EMB = false>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
     constexpr bool XREG = (MODE != GV_ORES) && B * (KCH / WK) <= 8;
     size_t lds = XREG ? 0 : (size_t)B * KCH * 512 * sizeof(uint16_t);
     static size_t attr = 0;  // largest dynamic LDS size granted so far
     if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH, EMB>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
     constexpr int per_block = (4 / WK) * RPW;
     int blocks = (a.n_units + per_block - 1) / per_block;
     if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
-    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_gemv<B, KCH, RPW, MODE, WK, XREG, DEPTH, EMB>), dim3(blocks), dim3(256), lds, s, a);
 }
 
 // K = 2048 (hidden); nh q heads, nkv kv heads of 256
+bool gemv_qkv_folds_embed(int B) { return B <= 2 && B < gemv_mf_min_batch(); }
+
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
-              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws) {
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws, const EmbedFold* emb) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wqkv; a.n_units = (nh + 2 * nkv) * 128; a.K = 2048; a.nb = B;
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;
+    if (emb) {  // layer 0: the token's embedding row is the input (and is written to h)
+        a.ids = emb->ids; a.E = emb->E; a.normalizer = emb->normalizer; a.pad_id = emb->pad_id; a.emb_out = emb->h_out;
+        const int cap = tune_variant("PGMI_QKV_CAP", 0);
+        if (B <= 1) launch_gemv<1, 4, 1, GV_QKV, 1, 1, true>(s, a, cap);
+        else launch_gemv<2, 4, 1, GV_QKV, 1, 1, true>(s, a);
+        return;
+    }
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
     if (B >= gemv_mf_min_batch()) {
         gemv_mf_qkv(s, a, ws);

@@ -44,10 +44,20 @@ struct StepState {  // device-resident decode step (read by kernels -> graph-rep
     int position;   // rotary position (= attention_mask.cumsum(-1)[:, -1], modeling_gemma.py:526)
 };
 
+// decode layer 0: the embedding lookup folded into the q|k|v GEMV (h_out receives the scaled row)
+struct EmbedFold {
+    const int64_t* ids;
+    const uint16_t* E;
+    float normalizer;
+    int64_t pad_id;
+    uint16_t* h_out;
+};
+bool gemv_qkv_folds_embed(int B);  // batches the fold covers (the register-input GEMV, B <= 2)
 // fused input RMSNorm + q/k/v projection + RoPE + KV-cache append (K = 2048)
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
-              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws = nullptr);
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws = nullptr,
+              const EmbedFold* emb = nullptr);
 // ws: fp32 scratch (>= 4 x B x N floats) for the MFMA path's K split of K = 16384 (B >= 3)
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
               float* ws);

@@ -771,10 +771,16 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
         EpiArgs q{};
         q.out = x->QKV; q.ldo = QKVN;
-        int sp = gemm(s, x->Tn, H, TL(x, i, "self_attn.q_proj.weight"), H, R, QKVN, H, EPI_STORE, q, x->ws,
-                      x->ws_bytes, 0, true);
-        rope_kv_append(s, x->QKV, x->ws, sp, B, L, NH, NKV, x->dpos, x->cosT, x->sinT, c.t_max_pos, x->Qr, Kc, Vc, kvb,
-                       kv_start);
+        // RoPE + KV append in the projection's epilogue where the shape's plan allows it
+        q.rpos = x->dpos; q.cosT = x->cosT; q.sinT = x->sinT; q.max_pos = c.t_max_pos;
+        q.q_out = x->Qr; q.kc = Kc; q.vc = Vc; q.kv_b_stride = kvb; q.kv_start = kv_start;
+        q.L = L; q.nh = NH; q.nkv = NKV;
+        const uint16_t* Wqkv = TL(x, i, "self_attn.q_proj.weight");
+        if (HD != 256 || !gemm_qkv_rope(s, x->Tn, H, Wqkv, H, R, QKVN, H, q)) {
+            int sp = gemm(s, x->Tn, H, Wqkv, H, R, QKVN, H, EPI_STORE, q, x->ws, x->ws_bytes, 0, true);
+            rope_kv_append(s, x->QKV, x->ws, sp, B, L, NH, NKV, x->dpos, x->cosT, x->sinT, c.t_max_pos, x->Qr, Kc, Vc,
+                           kvb, kv_start);
+        }
         AttnArgs a{};
         a.q = x->Qr; a.q_b_stride = (long)L * NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -785,7 +791,7 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         attention_prefill(s, 256, a);
         EpiArgs o{};
         o.res = x->Hs; o.ldr = H; o.out = x->Hs; o.ldo = H;
-        sp = gemm(s, x->AO, H, TL(x, i, "self_attn.o_proj.weight"), H, R, H, NH * HD, EPI_RES, o, x->ws, x->ws_bytes,
+        int sp = gemm(s, x->AO, H, TL(x, i, "self_attn.o_proj.weight"), H, R, H, NH * HD, EPI_RES, o, x->ws, x->ws_bytes,
                   0, true);
         splitk_res_norm(s, x->ws, sp, nullptr, x->Hs, TL(x, i, "post_attention_layernorm.weight"), nullptr, eps, x->Tn,
                         R, H);

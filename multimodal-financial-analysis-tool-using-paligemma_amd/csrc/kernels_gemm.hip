@@ -40,6 +40,14 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float
     }
 }
 
+// EPI_ROPE column map: a tile's logical column lr (wave lr / 32, 16-column tile (lr / 16) % 2, lane
+// lr % 16) reads weight row d or d + 128 of the same head, so the two tiles of a wave hold a rotary
+// pair (d, d + 128) in the same lane.  BN must divide 256 (a tile never straddles a head).
+__device__ __forceinline__ int rope_row(int n, int BN) {
+    const int h = n >> 8, u = n & 255, lr = u % BN;
+    return (h << 8) + ((lr >> 4) & 1) * 128 + (u / BN) * (BN / 2) + (lr >> 5) * 16 + (lr & 15);
+}
+
 // Epilogue of a wave's TM x TN MFMA tiles (C map of 16x16x32: column nb + 16 j + (lane & 15), rows
 // mb + 16 i + 4 (lane >> 4) + r).  Every operand the epilogue reads -- bias per column, residual /
 // position rows per element -- is loaded first from a clamped (always valid) address (epi_load),
@@ -133,6 +141,85 @@ __device__ __forceinline__ void epi_tile(const EpiArgs& ea, int M, int N, int mb
     EpiOps<EPI, TM, TN> e;
     epi_load<EPI, TM, TN>(ea, M, N, mb, nb, lane, e);
     epi_apply<EPI, TM, TN>(ea, M, N, mb, nb, lane, e, acc, acc2);
+}
+
+// EPI_ROPE epilogue of a wave's TM x 2 tiles (rope_row column map: the lane's tiles j = 0 / 1 are the
+// rotary pair (d, d + 128) of head h).  q|k|v round to bf16 first (the projections' outputs), then
+// q/k rotate with three roundings (modeling_gemma.py:197-198) exactly as k_rope_kv; v is copied.
+// rope_load reads the rows' positions (one batch), then their cos / sin (one batch); the kernels
+// call it before their k loops, so the two dependent round trips overlap the GEMM, and rope_apply
+// passes the values through one empty asm before its first store.
+template <int TM>
+struct RopeOps {
+    float cs[TM][4], sn[TM][4];
+    int h, d;
+};
+
+template <int TM, int BN>
+__device__ __forceinline__ void rope_load(const EpiArgs& ea, int M, int mb, int nbw, int lane, RopeOps<TM>& e) {
+    const int pr = rope_row(nbw + (lane & 15), BN);
+    e.h = pr >> 8;
+    e.d = pr & 255;  // < 128
+    long pv[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            m = m < M ? m : M - 1;
+            pv[i][r] = ea.rpos[m];
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(pv[i][r]));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            long p = pv[i][r];
+            p = p < 0 ? 0 : (p > ea.max_pos - 1 ? ea.max_pos - 1 : p);
+            e.cs[i][r] = bf2f(ea.cosT[p * 128 + e.d]);
+            e.sn[i][r] = bf2f(ea.sinT[p * 128 + e.d]);
+        }
+}
+
+template <int TM>
+__device__ __forceinline__ void rope_apply(const EpiArgs& ea, int M, int mb, int lane, RopeOps<TM>& e,
+                                           const f32x4 (&acc)[TM][2]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            asm volatile("" : "+v"(e.cs[i][r]));
+            asm volatile("" : "+v"(e.sn[i][r]));
+        }
+    const int h = e.h, d = e.d;
+    const bool rot = h < ea.nh + ea.nkv;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            if (m >= M) continue;
+            const float x0 = rbf(acc[i][0][r]), x1 = rbf(acc[i][1][r]);
+            const int b = m / ea.L, l = m - b * ea.L;
+            if (rot) {
+                const float c = e.cs[i][r], sv = e.sn[i][r];
+                const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sv));
+                const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sv));
+                uint16_t* dst;
+                if (h < ea.nh) dst = ea.q_out + (long)m * (ea.nh * 256) + h * 256;
+                else dst = ea.kc + b * ea.kv_b_stride + (long)(ea.kv_start + l) * (ea.nkv * 256) + (h - ea.nh) * 256;
+                dst[d] = o0;
+                dst[d + 128] = o1;
+            } else {
+                uint16_t* dst =
+                    ea.vc + b * ea.kv_b_stride + (long)(ea.kv_start + l) * (ea.nkv * 256) + (h - ea.nh - ea.nkv) * 256;
+                dst[d] = f2bf(x0);
+                dst[d + 128] = f2bf(x1);
+            }
+        }
 }
 
 // SPLIT: write raw fp32 partials to ws[z][M][N] (z = blockIdx.z) instead of the epilogue.
@@ -376,6 +463,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
             const int q = p - APC;
             const int bo = q / (BN / 8);
             row = n0 + (q % (BN / 8)) * 8 + prow;
+            if constexpr (EPI == EPI_ROPE) row = rope_row(row, BN);
             if (row > N - 1) row = N - 1;
             base = W + bo * up_off;
             ld = ldw;
@@ -438,6 +526,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     const int epi_mb = m0 + wm * TM * 16, epi_nb = n0 + wn * TN * 16;
     EpiOps<EPI, TM, TN> epi_ops;
     if constexpr (!SPLIT) epi_load<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops);
+    RopeOps<EPI == EPI_ROPE ? TM : 1> rope_ops;
+    if constexpr (!SPLIT && EPI == EPI_ROPE) rope_load<TM, BN>(ea, M, epi_mb, epi_nb, lane, rope_ops);
 
     // ring: tiles t+1 .. t+ST-1 in flight or landed while tile t is multiplied.  Per tile:
     //   read kk=1 fragments | MFMAs kk=0 | retire tile t+1, barrier, refill the slot tile t
@@ -495,6 +585,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
                     if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
+    } else if constexpr (EPI == EPI_ROPE) {
+        rope_apply<TM>(ea, M, epi_mb, lane, rope_ops, acc[0]);
     } else {
         epi_apply<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops, acc[0], acc[NB - 1]);
     }
@@ -565,6 +657,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
                 const int q = p - APC;
                 const int bo = q / (BN / 8);
                 row = n0 + (q % (BN / 8)) * 8 + prow;
+                if constexpr (EPI == EPI_ROPE) row = rope_row(row, BN);
                 if (row > N - 1) row = N - 1;
                 base = W + bo * up_off;
                 ld = ldw;
@@ -607,6 +700,8 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
 
     // ---------------- compute wave
     const int wm = wave / WN, wn = wave % WN;
+    RopeOps<EPI == EPI_ROPE ? TM : 1> rope_ops;
+    if constexpr (!SPLIT && EPI == EPI_ROPE) rope_load<TM, BN>(ea, M, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, rope_ops);
     f32x4 acc[NB][TM][TN];
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb)
@@ -653,6 +748,8 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
                     if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
+    } else if constexpr (EPI == EPI_ROPE) {
+        rope_apply<TM>(ea, M, m0 + wm * TM * 16, lane, rope_ops, acc[0]);
     } else {
         epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
     }
@@ -996,6 +1093,39 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
         case EPI_GEGLU: launch_e<EPI_GEGLU>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
     }
     return 1;
+}
+
+bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                   const EpiArgs& ea) {
+    static const bool off = [] {
+        const char* v = std::getenv("PGMI_QKV_ROPE");
+        return v && v[0] == '0';
+    }();
+    if (off || N % 256 != 0 || N != (ea.nh + 2 * ea.nkv) * 256) return false;
+    const Plan p = choose(M, N, K, false);
+    if (p.split != 1) return false;
+    // configurations with two 16-column tiles per wave and a tile width dividing 256
+#define P_(wm, tm, st) launch_p<4, wm, tm, 2, st, EPI_ROPE>(s, A, lda, W, ldw, M, N, K, ea, nullptr, 1, 0)
+#define W_(nw, tm, st) launch_w<nw, 2, tm, 2, st, 4, EPI_ROPE>(s, A, lda, W, ldw, M, N, K, ea, nullptr, 1, 0)
+    switch (p.cfg) {
+        case P288n: P_(2, 9, 3); break;
+        case P64x64: P_(2, 2, 6); break;
+        case P128x64: P_(2, 4, 6); break;
+        case P64x64s3: P_(2, 2, 3); break;
+        case P64x64s4: P_(2, 2, 4); break;
+        case P32x64s4: P_(2, 1, 4); break;
+        case P96x64s4: P_(2, 3, 4); break;
+        case P96x64s3: P_(2, 3, 3); break;
+        case W288w: W_(8, 9, 3); break;
+        case W64x64: W_(4, 2, 6); break;
+        case W352w: W_(8, 11, 2); break;
+        case W128x128: W_(8, 4, 4); break;
+        case W128x64: launch_w<4, 2, 4, 2, 5, 4, EPI_ROPE>(s, A, lda, W, ldw, M, N, K, ea, nullptr, 1, 0); break;
+        default: return false;
+    }
+#undef P_
+#undef W_
+    return true;
 }
 
 }  // namespace pgmi

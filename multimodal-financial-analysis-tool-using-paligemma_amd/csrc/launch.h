@@ -15,6 +15,8 @@ enum Epi : int {
     EPI_BIAS_POS = 5,   // out = bf16(bf16(acc + bias) + pos[m % npos])
     EPI_F32 = 6,        // out_f32 = float(bf16(acc))
     EPI_GEGLU = 7,      // out = bf16(bf16(gelu(bf16(acc_gate))) * bf16(acc_up))  (dual B)
+    EPI_ROPE = 8,       // Gemma q|k|v rows: RoPE on q and k, q -> q_out, k / v appended to the KV cache
+                        // (modeling_gemma.py:197-198,259); gemm_qkv_rope only
 };
 
 struct EpiArgs {
@@ -26,6 +28,20 @@ struct EpiArgs {
     uint16_t* out = nullptr;        // [M][ldo]
     int ldo = 0;
     float* out_f32 = nullptr;       // [M][ldo]
+    // EPI_ROPE: rows m = b * L + l at rotary position rpos[m]; heads [0, nh) are q (-> q_out
+    // [M][nh*256]), nh .. nh+nkv-1 are k, the rest v (-> kc / vc at token kv_start + l)
+    const int64_t* rpos = nullptr;
+    const uint16_t* cosT = nullptr;
+    const uint16_t* sinT = nullptr;
+    int max_pos = 0;
+    uint16_t* q_out = nullptr;
+    uint16_t* kc = nullptr;
+    uint16_t* vc = nullptr;
+    long kv_b_stride = 0;
+    int kv_start = 0;
+    int L = 1;
+    int nh = 0;
+    int nkv = 0;
 };
 
 // C[M,N] = A[M,K] (row-major, lda) x W[N,K]^T (row-major, ldw).  For EPI_GEGLU the
@@ -33,6 +49,11 @@ struct EpiArgs {
 // Returns the split-K factor used.  With defer = true and a split > 1 only the fp32 partial
 // slabs ws[split][M][N] are written and the epilogue is left to the consumer kernel
 // (splitk_res_norm / rope_kv_append); otherwise the epilogue is applied and 1 is returned.
+// q|k|v projection with the RoPE / KV-append epilogue (EPI_ROPE) when the measured plan for the
+// shape allows it (two 16-column tiles per wave, no split-K); false: nothing launched, the caller
+// runs gemm(EPI_STORE) + rope_kv_append
+bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                   const EpiArgs& ea);
 int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
          Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0, bool defer = false);
 size_t gemm_ws_bytes(int M, int N, int K);

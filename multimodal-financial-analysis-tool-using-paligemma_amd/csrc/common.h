@@ -29,11 +29,16 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
 
-// gelu(approximate="tanh") in fp32 (torch: 0.5*x*(1+tanh(sqrt(2/pi)*(x+0.044715*x^3))))
+// gelu(approximate="tanh") in fp32 (torch: 0.5*x*(1+tanh(sqrt(2/pi)*(x+0.044715*x^3)))), as the
+// identity 0.5*(1+tanh(u)) = 1/(1+exp(-2u)): one v_exp_f32 and one v_rcp_f32 (a few fp32 ulp, far
+// below the bf16 rounding that follows every use) instead of the library tanhf, whose branches and
+// division made the GELU epilogues of the fc1 / gate|up GEMMs cost up to a third of the kernel.
+// exp(-2u) overflowing to +inf gives x * 0 = -0 (gelu of a large negative x).
 __device__ __forceinline__ float gelu_tanh(float x) {
     const float k = 0.7978845608028654f;
-    float inner = k * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.0f + tanhf(inner));
+    const float u = k * (x + 0.044715f * x * x * x);
+    const float e = __builtin_amdgcn_exp2f(u * -2.8853900817779268f);  // exp(-2u) = 2^(-2u log2 e)
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -1087,7 +1087,7 @@ int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* strea
 }
 
 int pgmi_tune_gemm(int cfg, int split) {
-    if (cfg > 35 || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
+    if (cfg >= kGemmCfgs || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
     gemm_force_plan(cfg, split);
     return 0;
 }

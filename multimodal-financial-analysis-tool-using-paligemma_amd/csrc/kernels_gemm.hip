@@ -799,6 +799,7 @@ enum Cfg : int {
     W128x64 = 35,  // 2x2 compute waves, TM 4,  BN 64,  5 slots
     kNumCfg = 36,
 };
+static_assert(kNumCfg == kGemmCfgs, "launch.h kGemmCfgs");
 
 struct Plan {
     Cfg cfg;
@@ -839,7 +840,7 @@ static Plan choose(int M, int N, int K, bool dual) {
         {288, 2048, 16384, false, W288n, 8},    // text down             37.7 us
         {256, 3456, 1152, false, W64x64, 1},    // vision q|k|v          10.7 us
         {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        8.9 us
-        {256, 4304, 1152, false, P64x32s4, 1},  // vision fc1 (+GELU)    16.4 us (was split 3 + epilogue kernel)
+        {256, 4304, 1152, false, P96x64s4, 1},  // vision fc1 (+GELU)    11.0 us (exp/rcp GELU; was 16.4)
         {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            18.4 us
         {256, 1152, 640, false, P64x64, 1},     // patch embedding        7.5 us
         {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
@@ -849,7 +850,7 @@ static Plan choose(int M, int N, int K, bool dual) {
         {1056, 2048, 16384, false, W288w, 4},   // 448 px down           79.1 us (was 99.5 cold)
         {1024, 3456, 1152, false, W128x128, 1}, // 448 px vision q|k|v   18.3 us (was 24.6)
         {1024, 1152, 1152, false, P32x64s4, 1}, // 448 px vision out     12.0 us (was 22.8)
-        {1024, 4304, 1152, false, P64x64s3, 1}, // 448 px vision fc1     29.5 us (was 34.7)
+        {1024, 4304, 1152, false, W288w, 1},    // 448 px vision fc1     25.1 us (exp/rcp GELU; was 29.5)
         {1024, 1152, 4304, false, W128x128, 2}, // 448 px vision fc2     30.2 us (was 39.3)
         // configs[3]: 8 images per GPU as one batch (vision 2048 rows, text 2304 rows), cold sweep
         {2048, 3456, 1152, false, W288w, 1},    // vision q|k|v          31.2 us (was 46.8)

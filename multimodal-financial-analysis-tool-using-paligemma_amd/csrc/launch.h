@@ -58,6 +58,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
          Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0, bool defer = false);
 size_t gemm_ws_bytes(int M, int N, int K);
 void gemm_force_plan(int cfg, int split);  // cfg < 0: automatic
+constexpr int kGemmCfgs = 36;              // tile configurations (kernels_gemm.hip Cfg)
 
 // ---------------------------------------------------------------- decode GEMV
 struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)

@@ -22,6 +22,8 @@ SHAPES = {  # name: (M, N, K, epi)
     "t448_qkv": (1056, 2560, 2048, 0), "t448_o": (1056, 2048, 2048, 4), "t448_gateup": (1056, 16384, 2048, 7),
     "t448_down": (1056, 2048, 16384, 4), "v448_fc1": (1024, 4304, 1152, 2), "v448_qkv": (1024, 3456, 1152, 1),
     "v448_out": (1024, 1152, 1152, 3), "v448_fc2": (1024, 1152, 4304, 3),
+    # diagnostics: fc1 without the GELU (bias only), and with N padded to a multiple of 128
+    "v448_fc1_bias": (1024, 4304, 1152, 1), "v448_fc1_n4352": (1024, 4352, 1152, 2),
     # configs[3] prefill: 8 images per GPU as one batch (vision 8 x 256 rows, text 8 x 288 rows)
     "b8_v_qkv": (2048, 3456, 1152, 1), "b8_v_out": (2048, 1152, 1152, 3), "b8_v_fc1": (2048, 4304, 1152, 2),
     "b8_v_fc2": (2048, 1152, 4304, 3), "b8_v_proj": (2048, 2048, 1152, 1), "b8_t_qkv": (2304, 2560, 2048, 0),

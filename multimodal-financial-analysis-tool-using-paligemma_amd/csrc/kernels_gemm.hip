@@ -842,16 +842,16 @@ static Plan choose(int M, int N, int K, bool dual) {
         {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        8.9 us
         {256, 4304, 1152, false, P96x64s4, 1},  // vision fc1 (+GELU)    11.0 us (exp/rcp GELU; was 16.4)
         {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            18.4 us
-        {256, 1152, 640, false, P64x64, 1},     // patch embedding        7.5 us
+        {256, 1152, 640, false, P64x32s4, 1},   // patch embedding        5.3 us (was 6.6 on P64x64)
         {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
-        {1056, 2560, 2048, false, P96x64s3, 1}, // 448 px text q|k|v     18.8 us (was 24.1)
-        {1056, 2048, 2048, false, P96x64s3, 1}, // 448 px text o_proj    22.5 us (was 28.0)
+        {1056, 2560, 2048, false, W128x128, 1}, // 448 px text q|k|v     21.3 us (P96x64s3 24.0 in the same sweep)
+        {1056, 2048, 2048, false, W128x128, 1}, // 448 px text o_proj    19.5 us (P96x64s3 23.9)
         {1056, 16384, 2048, true, W352w, 1},    // 448 px gate|up       153.8 us (was 180.9 cold)
         {1056, 2048, 16384, false, W288w, 4},   // 448 px down           79.1 us (was 99.5 cold)
         {1024, 3456, 1152, false, W128x128, 1}, // 448 px vision q|k|v   18.3 us (was 24.6)
-        {1024, 1152, 1152, false, P32x64s4, 1}, // 448 px vision out     12.0 us (was 22.8)
+        {1024, 1152, 1152, false, P96x64s4, 1}, // 448 px vision out     10.6 us (P32x64s4 13.7)
         {1024, 4304, 1152, false, W288w, 1},    // 448 px vision fc1     25.1 us (exp/rcp GELU; was 29.5)
-        {1024, 1152, 4304, false, W128x128, 2}, // 448 px vision fc2     30.2 us (was 39.3)
+        {1024, 1152, 4304, false, W288w, 4},    // 448 px vision fc2     31.7 us (W128x128 split 2: 35.9)
         // configs[3]: 8 images per GPU as one batch (vision 2048 rows, text 2304 rows), cold sweep
         {2048, 3456, 1152, false, W288w, 1},    // vision q|k|v          31.2 us (was 46.8)
         {2048, 1152, 1152, false, W128x128, 1}, // vision out_proj       22.3 us (was 31.6)

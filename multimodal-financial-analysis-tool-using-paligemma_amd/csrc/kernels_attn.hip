@@ -40,7 +40,14 @@ __device__ __forceinline__ short8 load_frag(const uint16_t* rowp, bool /*row val
                                             int kk, int lane) {
     const int k = 32 * kk + 8 * (lane >> 4);
     if constexpr (HD % 32 == 0) return __builtin_bit_cast(short8, ldg16(rowp + k));
-    else return __builtin_bit_cast(short8, ldg16_sel(rowp + k, k < HD, rowp));
+    else {
+        // chunks past HD: an unconditional load of the row's first chunk (the address is selected,
+        // not the loaded value), zeroed by a mask -- no branch around the load
+        uint4 v = ldg16(rowp + (k < HD ? k : 0));
+        const unsigned msk = k < HD ? ~0u : 0u;
+        v.x &= msk; v.y &= msk; v.z &= msk; v.w &= msk;
+        return __builtin_bit_cast(short8, v);
+    }
 }
 
 typedef s4v_t s4v;
@@ -222,7 +229,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     constexpr int VS = HDP + 16;
     constexpr int CHK = 32;
     constexpr int VPT = (CHK * I::CH + 255) / 256;
-    static_assert(CHK * I::CH % 256 == 0, "every thread loads whole V chunks (no tail lanes)");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int LkP = (a.Lk + 31) & ~31;
     uint16_t* S = reinterpret_cast<uint16_t*>(smem_raw);  // [16][LkP] bf16 P
@@ -260,7 +266,8 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
-            const int e = tid + 256 * i;
+            int e = tid + 256 * i;
+            if (CHK * I::CH % 256 != 0 && e >= CHK * I::CH) e = 0;  // tail lanes (HD 72): re-read piece 0, not stored
             const int key = c * CHK + e / I::CH, ch = e % I::CH;
             vr[c][i] = ldg16(vbase + (long)(key < a.Lk ? key : a.Lk - 1) * a.v_row_stride + ch * 8);  // p = 0 past Lk
         }

@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
         if (tid < a.nb) {
             float m = bv[0][tid];
             int mi = bi[0][tid];
-            for (int q = 1; q < 4; ++q)
+            for (int q = 1; q < wpb; ++q)  // the workgroup's streaming waves, in a fixed order
                 if (bv[q][tid] > m || (bv[q][tid] == m && bi[q][tid] < mi)) { m = bv[q][tid]; mi = bi[q][tid]; }
             a.pmax[(long)tid * gridDim.x + blockIdx.x] = m;
             a.pidx[(long)tid * gridDim.x + blockIdx.x] = mi;
@@ -744,6 +744,8 @@ void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* ws) {
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
+    // (4 streaming waves with a 3-deep ring measured fastest: 2 waves x 5 / 7 deep and 1 wave x 8 deep,
+    // the same bytes in flight over fewer row streams, took the B = 8 step from 1.795 to 1.860-1.907 ms)
     if (env_int("PGMI_MF_ML", 1)) launch_ml<GV_GEGLU, 2, 2048, 3>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
     else launch_ms<GV_GEGLU, 2, 2048, 4>(s, a, ms_blocks(a.n_units, env_int("PGMI_MF_GU_CAP", 512)), 1, nullptr);
 }

@@ -114,7 +114,7 @@ def time_prefill(eng, px, ids, pos, kv, iters):
 
     def prefill():
         feats = eng.project(eng.vision(px))
-        lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
+        lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=2)
         return eng.argmax(lg[:, 0]), lg
 
     for _ in range(3):
@@ -132,7 +132,7 @@ def time_prefill(eng, px, ids, pos, kv, iters):
     e0.record()
     feats = eng.project(eng.vision(px))
     e1.record()
-    lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
+    lg = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=2)
     e2.record()
     e2.synchronize()
     return statistics.median(pre), e0.elapsed_time(e1), e1.elapsed_time(e2), lg
@@ -200,7 +200,7 @@ def time_no_kv(eng, px, ids, tokens):
         cur = ids
         for _ in range(tokens):
             feats = eng.project(eng.vision(px))
-            lg = eng.lm_forward(kv, 0, torch.arange(cur.shape[1])[None], ids=cur, image_feats=feats, logits_rows=1)
+            lg = eng.lm_forward(kv, 0, torch.arange(cur.shape[1])[None], ids=cur, image_feats=feats, logits_rows=2)
             cur = torch.cat([cur, eng.argmax(lg[:, 0])[:, None]], 1)
         return cur
     run()

@@ -118,7 +118,11 @@ int pgmi_embed(pgmi_ctx* ctx, const int64_t* ids, int rows, void* out, void* str
  *   positions: HOST int64 B x L (rotary positions, modeling_gemma.py:516-535).
  *   KV: keys/values of the L tokens are written at rows kv_start.. of the caller's slab;
  *   attention covers rows [0, kv_start + L) (the reference's zero mask: non-causal).
- *   logits (device fp32): logits_rows == 0 -> (B, L, vocab); 1 -> (B, 1, vocab) last row only. */
+ *   logits (device fp32): logits_rows == 0 -> (B, L, vocab); 1 -> (B, 1, vocab) last row only;
+ *   2 -> (B, 1, vocab) as 1, and no row but the last needs its final hidden state (the generate
+ *   loop, inference.py:55-63 takes logits[:, -1, :] only): the last layer writes every row's K/V,
+ *   then runs attention, o_proj, the MLP and the final norm for the last row alone (row-wise ops,
+ *   so the same values up to accumulation order); pgmi_lm_final_hidden then fails (PGMI_E_STATE). */
 int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, int n_img_rows, const void* embeds,
                     int B, int L, const int64_t* positions, void* kv, int kv_batch, int kv_max, int kv_start,
                     float* logits, int logits_rows, void* stream);

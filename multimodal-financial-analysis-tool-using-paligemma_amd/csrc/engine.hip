@@ -88,6 +88,7 @@ struct pgmi_ctx {
     uint16_t* sinT = nullptr;
     // text prefill workspace (rows = max_batch*max_seq)
     uint16_t *Hs, *Tn, *QKV, *Qr, *AO, *ACT, *lastrows;
+    long tn_rows = 0;  // rows of Tn holding the final RMSNorm of the last pgmi_lm_forward (pgmi_lm_final_hidden)
     int64_t* dpos;
     int64_t* dids_tmp;
     // vision workspace (rows = max_batch*N)
@@ -730,6 +731,7 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
     if (L < 1 || L > c.max_seq) return fail(PGMI_E_ARG, "sequence length exceeds max_seq");
     if (kv_start < 0 || kv_start + L > kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
     if (!positions || !kv || !logits || (!embeds && !ids)) return fail(PGMI_E_ARG, "null argument");
+    if (logits_rows < 0 || logits_rows > 2) return fail(PGMI_E_ARG, "logits_rows must be 0, 1 or 2");
     // host positions -> device (outside any graph: a pageable host copy is not captured)
     HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)B * L * sizeof(int64_t), hipMemcpyHostToDevice,
                           (hipStream_t)stream));
@@ -740,6 +742,7 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
                        logits_rows);
     });
     if (rc) return rc;
+    x->tn_rows = logits_rows == 2 && L > 1 ? 0 : (long)B * L;
     LAUNCHCHK();
     return 0;
 }
@@ -763,6 +766,7 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
     const uint16_t* fnorm = W(x, "language_model.model.norm.weight");
+    const bool last_only = logits_rows == 2 && L > 1 && c.t_layers > 0;
     // input RMSNorm of layer 0; every later RMSNorm (and the final norm) is fused with the
     // preceding projection's split-K reduction + residual (splitk_res_norm)
     rmsnorm(s, x->Hs, c.t_layers ? TL(x, 0, "input_layernorm.weight") : fnorm, eps, x->Tn, R, H);
@@ -788,6 +792,24 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         a.o = x->AO; a.o_b_stride = (long)L * H; a.o_row_stride = H; a.o_head_stride = HD;
         a.Lq = L; a.Lk = kv_start + L; a.G = NH / NKV; a.n_kv = NKV; a.B = B;
         a.scale = 1.0f / std::sqrt((float)HD);  // / math.sqrt(head_dim) (:266): exact power of two
+        if (last_only && i + 1 == c.t_layers) {
+            // logits_rows == 2, last layer: the K/V rows of every token are written above (the cache
+            // the decode loop reads); the rest of the layer feeds only the final hidden state, and the
+            // caller reads that for the last row alone, so attention, o_proj, the MLP and the final
+            // norm run for the last row of each sequence (row-wise ops: the same values as the
+            // all-row pass up to GEMV-vs-GEMM accumulation order), on the decode GEMVs
+            a.q = x->Qr + (size_t)(L - 1) * NH * HD;
+            a.o = x->dAO; a.o_b_stride = (long)H;
+            a.Lq = 1;
+            attention_prefill(s, 256, a);
+            HIPCHK(hipMemcpy2DAsync(x->lastrows, (size_t)H * 2, x->Hs + (size_t)(L - 1) * H, (size_t)L * H * 2,
+                                    (size_t)H * 2, B, hipMemcpyDeviceToDevice, s));
+            gemv_res(s, B, NH * HD, x->dAO, TL(x, i, "self_attn.o_proj.weight"), H, x->lastrows, x->ws);
+            gemv_geglu(s, B, x->lastrows, TL(x, i, "post_attention_layernorm.weight"), eps,
+                       TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);
+            gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->lastrows, x->ws);
+            break;
+        }
         attention_prefill(s, 256, a);
         EpiArgs o{};
         o.res = x->Hs; o.ldr = H; o.out = x->Hs; o.ldo = H;
@@ -812,8 +834,9 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         l.out_f32 = logits; l.ldo = c.t_vocab;
         gemm(s, x->Tn, H, E, H, R, c.t_vocab, H, EPI_F32, l, x->ws, x->ws_bytes);
     } else {
-        HIPCHK(hipMemcpy2DAsync(x->lastrows, (size_t)H * 2, x->Hs + (size_t)(L - 1) * H, (size_t)L * H * 2,
-                                (size_t)H * 2, B, hipMemcpyDeviceToDevice, s));
+        if (!last_only)
+            HIPCHK(hipMemcpy2DAsync(x->lastrows, (size_t)H * 2, x->Hs + (size_t)(L - 1) * H, (size_t)L * H * 2,
+                                    (size_t)H * 2, B, hipMemcpyDeviceToDevice, s));
         int nparts = 0;
         gemv_logits(s, B, x->lastrows, fnorm, eps, E, c.t_vocab, logits, x->pmax, x->pidx, &nparts);
     }
@@ -950,6 +973,8 @@ int pgmi_lm_final_hidden(pgmi_ctx* x, void* out, int rows, void* stream) {
     if ((rc = ensure_prepared(x))) return rc;
     if (!out) return fail(PGMI_E_ARG, "null argument");
     if (rows < 1 || rows > x->c.max_batch * x->c.max_seq) return fail(PGMI_E_ARG, "rows exceed the prefill workspace");
+    if (rows > x->tn_rows)
+        return fail(PGMI_E_STATE, "the last pgmi_lm_forward did not keep these rows' final hidden states (logits_rows 2)");
     HIPCHK(hipMemcpyAsync(out, x->Tn, (size_t)rows * x->c.t_hidden * 2, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return 0;
 }

@@ -233,7 +233,9 @@ class Engine:
     def lm_forward(self, kv: torch.Tensor, kv_start: int, positions, ids=None, image_feats=None, embeds=None,
                    logits_rows: int = 0) -> torch.Tensor:
         """GemmaForCausalLM.forward over merged embeddings (see pgmi.h).  Returns fp32 logits
-        (B, L, V) or (B, 1, V)."""
+        (B, L, V) (logits_rows 0) or (B, 1, V): logits_rows 1 keeps every row's final hidden state
+        for final_hidden / lazy all-row logits; 2 needs only the last row's, so the last layer's
+        post-attention work runs for the last row alone (the KV cache is written for every row)."""
         self._ready()
         if embeds is not None:
             e = embeds.to(self.device, torch.bfloat16).contiguous()
@@ -339,7 +341,7 @@ class Engine:
         if kv is None:
             kv = self.new_kv(B, L + n_tokens + 1)
         feats = self.project(self.vision(pixel_values))
-        logits = self.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=1)
+        logits = self.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=2)
         toks = torch.empty((B, n_tokens), dtype=torch.int64, device=self.device)
         if do_sample:
             us = torch.rand((n_tokens, B), device=self.device, generator=generator)

@@ -101,6 +101,7 @@ struct pgmi_ctx {
     int *pidx, *amax_i;
     int max_chunks;
     StepState* step;
+    StepState* pstep;  // the generate-loop prefill's last-row attention (flash-decoding over the prompt's keys)
     int64_t* d_ids;
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
@@ -549,6 +550,7 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->dlogits, (size_t)B * c.t_vocab))) return rc;
         if ((rc = dalloc_t(x, &x->pidx, (size_t)B * gemv_logits_blocks()))) return rc;
         if ((rc = dalloc_t(x, &x->step, 1))) return rc;
+        if ((rc = dalloc_t(x, &x->pstep, 1))) return rc;
         if ((rc = dalloc_t(x, &x->amax_v, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
@@ -801,10 +803,22 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
             a.q = x->Qr + (size_t)(L - 1) * NH * HD;
             a.o = x->dAO; a.o_b_stride = (long)H;
             a.Lq = 1;
-            attention_prefill(s, 256, a);
             HIPCHK(hipMemcpy2DAsync(x->lastrows, (size_t)H * 2, x->Hs + (size_t)(L - 1) * H, (size_t)L * H * 2,
                                     (size_t)H * 2, B, hipMemcpyDeviceToDevice, s));
-            gemv_res(s, B, NH * HD, x->dAO, TL(x, i, "self_attn.o_proj.weight"), H, x->lastrows, x->ws);
+            if (kv_start + L <= c.max_kv) {
+                // one query row over the prompt's keys: the decode step's flash-decoding (64-key chunks
+                // in parallel, kv_len from a device step record set by a memset node) and its o_proj
+                // GEMV with the chunk combine in the prologue; a single 16-row prefill workgroup
+                // would walk every key alone
+                a.Lk = 0;
+                HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x->pstep->kv_len), kv_start + L - 1, 1, s));
+                attention_decode(s, a, x->pstep, kv_start + L, x->opart, x->max_chunks);
+                gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->pstep, TL(x, i, "self_attn.o_proj.weight"), H,
+                            x->lastrows, B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+            } else {
+                attention_prefill(s, 256, a);
+                gemv_res(s, B, NH * HD, x->dAO, TL(x, i, "self_attn.o_proj.weight"), H, x->lastrows, x->ws);
+            }
             gemv_geglu(s, B, x->lastrows, TL(x, i, "post_attention_layernorm.weight"), eps,
                        TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);
             gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->lastrows, x->ws);

@@ -88,9 +88,10 @@ def test_last_row_only_final_layer(eng, gold, B):
     torch.cuda.synchronize()
     assert torch.equal(kv1[:, :, :, :L], kv2[:, :, :, :L])
     for b in range(B):
-        # one layer's attention / o_proj / MLP on other kernels (decode GEMVs vs prefill GEMMs):
-        # accumulation order, then bf16 rounding of the residual stream (measured 1.9e-3)
-        assert rel_l2(l2[b].cpu().numpy(), l1[b].cpu().numpy()) < 5e-3
+        # one layer (of this model's two) on the decode kernels: GEMV-vs-GEMM accumulation order,
+        # flash-decoding's chunk-local bf16 p, then bf16 rounding of the residual
+        # stream (measured 1.9e-3 at B = 1, 5.1e-3 at B = 3 on the MFMA GEMVs)
+        assert rel_l2(l2[b].cpu().numpy(), l1[b].cpu().numpy()) < 1e-2
         assert int(l2[b].argmax()) == int(l1[b].argmax())
     assert torch.isfinite(h1).all()
     with pytest.raises(AssertionError):

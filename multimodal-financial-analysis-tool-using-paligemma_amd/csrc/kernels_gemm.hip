@@ -712,6 +712,59 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
     const int swz = lane & 7;
     const int arow0 = (wm * TM * 16 + (lane & 15)) * 128;
     const int brow0 = ABYTES + (wn * TN * 16 + (lane & 15)) * 128;
+#ifndef PGMI_GEMM_W_PIPE
+#define PGMI_GEMM_W_PIPE 1
+#endif
+    // (two fragment sets: taller wave tiles than TM 9 spill at three waves per SIMD)
+    constexpr bool PIPE = PGMI_GEMM_W_PIPE && TM <= 9 && EPI != EPI_ROPE;  // (RoPE epilogue: its operands spill)
+    if constexpr (PIPE) {
+    // Fragment reads pipelined across the barrier (k_gemm_p's schedule): per tile t,
+    //   read kk=1 fragments of t | MFMAs kk=0 | lgkmcnt(0), barrier t+1 (tile t+1 landed; the loaders
+    //   may now refill t's slot: its fragments are all in registers) | read kk=0 fragments of t+1 |
+    //   MFMAs kk=1 of t
+    // so the LDS latency of a tile's first fragments hides behind the previous tile's second MFMA
+    // block, and a wave's barrier wait overlaps nothing but its own issued reads.  The loader side is
+    // unchanged: nkt barriers in all (one before the loop, one inside each iteration but the last).
+    short8 fa0[TM], fb0[NB][TN], fa1[TM], fb1[NB][TN];
+#define PGMI_W_READ(FA, FB, SB, KK)                                                                        \
+    do {                                                                                                   \
+        const int ch_ = ((((KK) * 4) + (lane >> 4)) ^ swz) << 4;                                           \
+        _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) FA[i_] =                                         \
+            *reinterpret_cast<const short8*>((SB) + arow0 + i_ * 16 * 128 + ch_);                          \
+        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
+            FB[b_][j_] = *reinterpret_cast<const short8*>((SB) + brow0 + (b_ * BN + j_ * 16) * 128 + ch_); \
+    } while (0)
+#define PGMI_W_MFMA(FA, FB)                                                                                \
+    do {                                                                                                   \
+        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) \
+            _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) acc[b_][i_][j_] =                             \
+                mfma16(FA[i_], FB[b_][j_], acc[b_][i_][j_]);                                               \
+    } while (0)
+    int slot = 0;
+    if (nkt > 0) {
+        __builtin_amdgcn_s_barrier();  // tile 0 is in slot 0
+        PGMI_W_READ(fa0, fb0, smem_w, 0);
+    }
+    for (int t = 0; t < nkt; ++t) {
+        const uint8_t* sb = smem_w + slot * SBYTES;
+        PGMI_W_READ(fa1, fb1, sb, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        PGMI_W_MFMA(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        slot = slot + 1 == ST ? 0 : slot + 1;
+        if (t + 1 < nkt) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): tile t's fragments are in registers
+            __builtin_amdgcn_s_barrier();        // tile t+1 is in slot `slot`
+            __builtin_amdgcn_sched_barrier(0);
+            PGMI_W_READ(fa0, fb0, smem_w + slot * SBYTES, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        PGMI_W_MFMA(fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#undef PGMI_W_READ
+#undef PGMI_W_MFMA
+    } else {
     short8 fa[TM], fb[NB][TN];
     int slot = 0;
     for (int t = 0; t < nkt; ++t) {
@@ -735,6 +788,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
                     for (int j = 0; j < TN; ++j) acc[bb][i][j] = mfma16(fa[i], fb[bb][j], acc[bb][i][j]);
         }
         slot = slot + 1 == ST ? 0 : slot + 1;
+    }
     }
     if constexpr (SPLIT) {
 #pragma unroll

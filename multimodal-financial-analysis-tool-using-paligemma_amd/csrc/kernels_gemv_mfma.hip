@@ -132,8 +132,16 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     const int k0 = (ks * WK + wk) * KW;
     const int n_groups = (a.n_units + 15) / 16;
 
+    // GV_QKV, NR 2: unit u = rotary pair (d, d + 128) of head u >> 7 in one lane (two row sets).
+    // GV_QKV, NR 1: unit u = one weight row; a 16-row group is 8 rotary pairs of one head, d in lanes
+    // n < 8 and d + 128 in lane n + 8 (the partner value is one lane swap away in the C map), so the
+    // 2,560 rows make 160 groups (twice the workgroups of the pair form)
     auto row_of = [&](int u, int j) -> long {
-        if constexpr (MODE == GV_QKV) return (long)((u >> 7) * 256 + (u & 127) + j * 128);
+        if constexpr (MODE == GV_QKV && NR == 2) return (long)((u >> 7) * 256 + (u & 127) + j * 128);
+        else if constexpr (MODE == GV_QKV) {
+            const int grp_ = u >> 4, nn = u & 15;
+            return (long)((grp_ >> 4) * 256 + (grp_ & 15) * 8 + (nn & 7) + (nn >> 3) * 128);
+        }
         else if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
         else return (long)u;
     };
@@ -158,7 +166,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     if constexpr (MODE == GV_QKV) {
         int p0 = a.st->position;
         p0 = p0 < 0 ? 0 : (p0 > a.max_pos - 1 ? a.max_pos - 1 : p0);
-        const int d0 = (grp * 16 + n) & 127;
+        const int d0 = NR == 2 ? ((grp * 16 + n) & 127) : ((grp & 15) * 8 + (n & 7));
         cs0 = bf2f(a.cosT[(long)p0 * 128 + d0]);
         sn0 = bf2f(a.sinT[(long)p0 * 128 + d0]);
     }
@@ -226,6 +234,32 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
         }
         // C map: col n = unit (cur*16 + n), row b = 4g + r
         const int u = cur * 16 + n;
+        if constexpr (MODE == GV_QKV && NR == 1) {
+            // the rotary partner of this lane's row is lane n ^ 8's (same rows b)
+            f32x4 part;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[r] = __shfl_xor(acc[0][r], 8, 64);
+            const int hh = cur >> 4, d = (cur & 15) * 8 + (n & 7), hi = n >> 3;
+            const int nh = a.I;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int b = 4 * g + r;
+                if (b >= a.nb) break;
+                const float x0 = rbf(hi ? part[r] : acc[0][r]), x1 = rbf(hi ? acc[0][r] : part[r]);
+                if (hh < nh + a.nkv) {
+                    const float c = cur == grp0 ? cs0 : bf2f(a.cosT[(long)pos * 128 + d]);
+                    const float sn = cur == grp0 ? sn0 : bf2f(a.sinT[(long)pos * 128 + d]);
+                    const uint16_t o = hi ? f2bf(rbf(x1 * c) + rbf(x0 * sn)) : f2bf(rbf(x0 * c) + rbf(-x1 * sn));
+                    uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256
+                                            : a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
+                    dst[d + hi * 128] = o;
+                } else {
+                    uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh - a.nkv) * 256;
+                    dst[d + hi * 128] = f2bf(hi ? x1 : x0);
+                }
+            }
+            continue;
+        }
         if (u >= a.n_units) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -732,7 +766,13 @@ static int ms_blocks(int units, int cap) {
 // would leave most CUs idle), fp32 partials in ws, then RoPE + KV append in k_mf_qkv_rope
 void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* ws) {
     if (!ws || env_int("PGMI_MF_QKV_SPLIT", 0) == 0) {  // default: the in-workgroup K split form (measured faster)
-        launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
+        if (env_int("PGMI_MF_QKV_ROWS", 1)) {  // one row per lane, rotary pairs across lanes: 160 workgroups
+            GemvArgs r = a;
+            r.n_units = 2 * a.n_units;
+            launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
+        } else {
+            launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
+        }
         return;
     }
     constexpr int KS = 4;

@@ -797,6 +797,13 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     GemvArgs r = a;
     r.x = o;
     r.norm_w = nullptr;
+    // 128 workgroups of 8 waves splitting K (the q|k|v form) instead of 64 two-wave LDS-ring workgroups:
+    // B = 8 step 1.751-1.760 -> 1.718-1.721 ms (same-box A/B); PGMI_MF_O_MF=0 restores the ring form.
+    // (The same form for the K = 16384 down projection, 1,024 workgroups, measured slower: 1.79 ms.)
+    if (env_int("PGMI_MF_O_MF", 1)) {
+        launch_mf<GV_RES, 1, 256, 8>(s, r, groups_of(a.n_units), 1, nullptr);
+        return;
+    }
     if (env_int("PGMI_MF_ML", 1)) {
         // 2048 rows = 128 groups of 16: 4-wave workgroups would occupy only 32 CUs
         static const int w = env_int("PGMI_MF_O_WAVES", 2);  // measured: 4 -> 1.828, 1 -> 1.812, 2 -> 1.807 ms per B = 8 step

@@ -135,6 +135,15 @@ int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, 
  *   argmax back in place (tokens are read first, the next ones written last): no staging copy. */
 int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                 int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
+/* The same decode step with already-merged input rows instead of token ids: embeds (device bf16
+ * [B][hidden]) is the output of a caller's _merge_input_ids_with_image_features for a q_len == 1
+ * step (the ablation harness monkey-patches the merge, ablation_study_fixed.py:99-142,335-337,
+ * and then calls forward(input_ids=next_token, pixel_values=None, ...) per token, :215-221);
+ * the rows are scaled by bf16(sqrt(hidden)) (GemmaModel, modeling_gemma.py:367-368) and run
+ * through the same (graph-replayed) step.  The rows are staged into a context buffer first, so
+ * the caller's buffer may change between calls. */
+int pgmi_decode_embeds(pgmi_ctx* ctx, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                       int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
 /* Prefill graphs (default on): pgmi_vision and pgmi_lm_forward replay a captured hipGraph when
  * called again with identical pointer and size arguments (the graph is captured on the second
  * such call; a replay reads the same addresses as the eager call would).  0 = always eager. */
@@ -196,13 +205,8 @@ int pgmi_tune_gemm(int cfg, int split);
 
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
  * LDS-resident scores, 8 = the same with every K/V load issued up front (head_dim 256, <= 320 keys), RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
- * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); 91, 92, 94 = K/V resident in LDS with 1, 2, 4
- * waves of 16 query rows (short key ranges only); -1 restores the measured choice. */
+ * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); -1 restores the measured choice. */
 int pgmi_tune_attention(int variant);
-
-/* Diagnostics: copy the in-kernel phase stamps (100 MHz real-time counter, [slot][8 phases][64 lanes])
- * of the last stamped diagnostic kernel variant (which = 0: prefill attention variant 9) to host. */
-int pgmi_debug_stamps(int which, long long* host, long n_words);
 
 /* Nucleus sampling, inference.py:15-24 (_sample_top_p) with inference.py:65's
  * softmax(logits / temperature) fused when temperature > 0 (temperature <= 0: x already holds

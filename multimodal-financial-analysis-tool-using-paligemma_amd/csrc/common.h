@@ -86,15 +86,4 @@ __device__ __forceinline__ f32x4 mfma16(const short8 a, const short8 b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// ---- diagnostics: in-kernel phase stamps (diagnostic kernel variants only; never in a product
-// launch).  Every lane of wave 0 stores the 100 MHz real-time counter at a phase boundary into
-// buf[(slot * kStampPhases + phase) * 64 + lane] with a vector store (divergent address); each
-// translation unit that stamps owns its buffer and a host read-back (pgmi_debug_stamps).
-constexpr int kStampPhases = 8, kStampSlots = 512;
-constexpr long kStampWords = (long)kStampSlots * kStampPhases * 64;
-__device__ __forceinline__ void stamp_to(long long* buf, int slot, int phase) {
-    if (threadIdx.x < 64 && slot < kStampSlots)
-        buf[((long)slot * kStampPhases + phase) * 64 + threadIdx.x] = (long long)wall_clock64();
-}
-
 }  // namespace pgmi

@@ -16,7 +16,9 @@
 #include <unordered_map>
 #include <vector>
 
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+
+#include <rccl/rccl.h>  // types only: librccl is dlopen'ed on first use
 
 #include "../../include/pgmi.h"
 #include "common.h"
@@ -59,9 +61,10 @@ struct GraphKey {
     float* logits;
     int64_t* next;
     const int64_t* ids;  // the ids buffer the graph reads (the context's staging copy, or in place)
+    bool emb;            // the step's input is the staged embedding rows (pgmi_decode_embeds), not ids
     bool operator<(const GraphKey& o) const {
-        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids) <
-               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids);
+        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids, emb) <
+               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids, o.emb);
     }
 };
 
@@ -103,6 +106,7 @@ struct pgmi_ctx {
     StepState* step;
     StepState* pstep;  // the generate-loop prefill's last-row attention (flash-decoding over the prompt's keys)
     int64_t* d_ids;
+    uint16_t* d_emb;             // staged input rows of pgmi_decode_embeds ([max_batch][hidden] bf16)
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
     hipStream_t cap_stream = nullptr;
@@ -269,6 +273,37 @@ int ensure_prepared(pgmi_ctx* x) {
 }  // namespace
 
 // ================================================================ C ABI
+// RCCL is loaded on first use (dlopen), so a single-GPU process -- and the CPU tests that only load
+// the library -- need no librccl; the four entry points it uses are resolved once.
+namespace {
+struct Rccl {
+    bool tried = false;
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    if (!r.tried) {
+        r.tried = true;
+        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (r.h) {
+            r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(r.h, "ncclGetUniqueId"));
+            r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.h, "ncclCommInitRank"));
+            r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.h, "ncclCommDestroy"));
+            r.broadcast = reinterpret_cast<decltype(r.broadcast)>(dlsym(r.h, "ncclBroadcast"));
+            r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.h, "ncclGetErrorString"));
+        }
+    }
+    return r;
+}
+}  // namespace
+
 extern "C" {
 
 const char* pgmi_last_error(void) { return g_err.c_str(); }
@@ -554,6 +589,7 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->amax_v, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
+        if ((rc = dalloc_t(x, &x->d_emb, (size_t)B * H))) return rc;
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
@@ -737,6 +773,8 @@ int pgmi_lm_forward(pgmi_ctx* x, const int64_t* ids, const void* image_feats, in
     // host positions -> device (outside any graph: a pageable host copy is not captured)
     HIPCHK(hipMemcpyAsync(x->dpos, positions, (size_t)B * L * sizeof(int64_t), hipMemcpyHostToDevice,
                           (hipStream_t)stream));
+    // Tn is overwritten from here on: no row of it is valid until this call has succeeded
+    x->tn_rows = 0;
     const std::vector<intptr_t> key{2, (intptr_t)ids, (intptr_t)image_feats, n_img_rows, (intptr_t)embeds, B, L,
                                     (intptr_t)kv, kv_batch, kv_max, kv_start, (intptr_t)logits, logits_rows};
     rc = run_graphed(x, (hipStream_t)stream, key, [&](hipStream_t st) {
@@ -859,7 +897,7 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
 }
 
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
-                       int launch_keys, float* logits, int64_t* next_ids) {
+                       int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr) {
     const pgmi_config& c = x->c;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const float eps = c.t_rms_eps;
@@ -868,13 +906,11 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const long kvd = (long)NKV * HD, kvb = (long)kv_max * kvd;
     uint16_t* kvp = reinterpret_cast<uint16_t*>(kv);
     // B <= 2: the embedding row is read by layer 0's q|k|v GEMV itself (one launch fewer per step)
-    static const bool fold_env = [] {
-        const char* e = std::getenv("PGMI_EMBED_FOLD");
-        return !e || std::atoi(e) != 0;
-    }();
-    const bool fold = fold_env && gemv_qkv_folds_embed(B) && c.t_layers > 0;
+    const bool fold = !embeds && gemv_qkv_folds_embed(B) && c.t_layers > 0;
     const EmbedFold emb{ids, E, normalizer, c.pad_token_id, x->dH};
-    if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
+    if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
+    else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
@@ -910,15 +946,15 @@ int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {
     return 0;
 }
 
-int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len, int position,
-                float* logits, int64_t* next_ids, int use_graph, void* stream) {
+static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int B, void* kv, int kv_batch, int kv_max,
+                       int kv_len, int position, float* logits, int64_t* next_ids, int use_graph, void* stream) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;
     const pgmi_config& c = x->c;
     if (B < 1 || B > c.max_batch || B > kv_batch) return fail(PGMI_E_ARG, "batch exceeds capacity");
     if (kv_len < 0 || kv_len >= kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
-    if (!ids || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
+    if ((!ids && !embeds) || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
     if (!x->step_known || x->step_kv != kv_len || x->step_pos != position) set_step(s, x->step, kv_len, position);
     // the step advances the device state itself (its last kernel); known only once this call has
@@ -929,8 +965,14 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         x->step_kv = kv_len + 1;
         x->step_pos = position + 1;
     };
+    // input rows are always staged into the context's buffer (a stable address the graph reads)
+    const uint16_t* erows = nullptr;
+    if (embeds) {
+        HIPCHK(hipMemcpyAsync(x->d_emb, embeds, (size_t)B * c.t_hidden * 2, hipMemcpyDeviceToDevice, s));
+        erows = x->d_emb;
+    }
     if (!use_graph) {
-        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids))) return rc;
+        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids, erows))) return rc;
         LAUNCHCHK();
         advanced();
         return 0;
@@ -938,15 +980,16 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     // in-place feedback (next_ids == ids: the step reads its tokens first and writes the next
     // ones last) needs no staging copy; other callers' ids are staged into the context's buffer
     const int64_t* gids = ids;
-    if (ids != next_ids) {
+    if (!embeds && ids != next_ids) {
         HIPCHK(hipMemcpyAsync(x->d_ids, ids, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         gids = x->d_ids;
     }
-    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids};
+    if (embeds) gids = nullptr;
+    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids, embeds != nullptr};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids))) return rc;
+            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows))) return rc;
             LAUNCHCHK();
             advanced();
             return 0;
@@ -954,7 +997,7 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids);
+        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
         if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
@@ -964,6 +1007,19 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
     LAUNCHCHK();
     advanced();
     return 0;
+}
+
+int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len, int position,
+                float* logits, int64_t* next_ids, int use_graph, void* stream) {
+    if (!ids) return fail(PGMI_E_ARG, "null argument");
+    return decode_step(x, ids, nullptr, B, kv, kv_batch, kv_max, kv_len, position, logits, next_ids, use_graph, stream);
+}
+
+int pgmi_decode_embeds(pgmi_ctx* x, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                       int position, float* logits, int64_t* next_ids, int use_graph, void* stream) {
+    if (!embeds) return fail(PGMI_E_ARG, "null argument");
+    return decode_step(x, nullptr, embeds, B, kv, kv_batch, kv_max, kv_len, position, logits, next_ids, use_graph,
+                       stream);
 }
 
 int pgmi_lm_head(pgmi_ctx* x, const void* normed, int rows, float* logits, void* stream) {
@@ -994,17 +1050,25 @@ int pgmi_lm_final_hidden(pgmi_ctx* x, void* out, int rows, void* stream) {
 }
 
 // ---------------------------------------------------------------- replicas: load-time broadcast
+#define RCCL_READY()                                                                       \
+    do {                                                                                   \
+        const Rccl& r_ = rccl();                                                           \
+        if (!r_.get_unique_id || !r_.comm_init_rank || !r_.comm_destroy || !r_.broadcast || !r_.error_string) \
+            return fail(PGMI_E_STATE, "librccl could not be loaded (dlopen librccl.so.1)");  \
+    } while (0)
+
 #define NCCLCHK(expr)                                                                      \
     do {                                                                                   \
         ncclResult_t r_ = (expr);                                                          \
-        if (r_ != ncclSuccess) return fail(PGMI_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+        if (r_ != ncclSuccess) return fail(PGMI_E_HIP, std::string(#expr) + ": " + rccl().error_string(r_)); \
     } while (0)
 
 int pgmi_comm_unique_id(void* id_out) {
     if (!id_out) return fail(PGMI_E_ARG, "null argument");
+    RCCL_READY();
     static_assert(sizeof(ncclUniqueId) == PGMI_COMM_ID_BYTES, "ncclUniqueId size");
     ncclUniqueId id;
-    NCCLCHK(ncclGetUniqueId(&id));
+    NCCLCHK(rccl().get_unique_id(&id));
     std::memcpy(id_out, &id, sizeof(id));
     return 0;
 }
@@ -1012,28 +1076,41 @@ int pgmi_comm_unique_id(void* id_out) {
 int pgmi_comm_init(int device, int nranks, int rank, const void* id, void** comm_out) {
     if (!id || !comm_out) return fail(PGMI_E_ARG, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PGMI_E_ARG, "bad rank / world size");
+    RCCL_READY();
+    // the communicator binds to the current device: switch for the init, then give the caller's
+    // thread its own current device back (torch keeps its own notion of it)
+    int prev = 0;
+    HIPCHK(hipGetDevice(&prev));
     HIPCHK(hipSetDevice(device));
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
     ncclComm_t comm = nullptr;
-    NCCLCHK(ncclCommInitRank(&comm, nranks, uid, rank));
+    const ncclResult_t r = rccl().comm_init_rank(&comm, nranks, uid, rank);
+    HIPCHK(hipSetDevice(prev));
+    if (r != ncclSuccess) return fail(PGMI_E_HIP, std::string("ncclCommInitRank: ") + rccl().error_string(r));
     *comm_out = comm;
     return 0;
 }
 
 int pgmi_comm_destroy(void* comm) {
     if (!comm) return 0;
-    NCCLCHK(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+    RCCL_READY();
+    NCCLCHK(rccl().comm_destroy(reinterpret_cast<ncclComm_t>(comm)));
     return 0;
 }
 
 int pgmi_broadcast_weights(pgmi_ctx* x, void* comm, int root, void* stream) {
     if (!x || !comm) return fail(PGMI_E_ARG, "null argument");
     if (!x->slab) return fail(PGMI_E_STATE, "weights are not bound (pgmi_bind_weights)");
+    RCCL_READY();
+    int prev = 0;
+    HIPCHK(hipGetDevice(&prev));
     HIPCHK(hipSetDevice(x->device));
     // the whole slab in one in-place collective: rank `root`'s bytes land in every replica
-    NCCLCHK(ncclBroadcast(x->slab, x->slab, (size_t)x->slab_bytes, ncclUint8, root, reinterpret_cast<ncclComm_t>(comm),
-                          (hipStream_t)stream));
+    const ncclResult_t r = rccl().broadcast(x->slab, x->slab, (size_t)x->slab_bytes, ncclUint8, root,
+                                            reinterpret_cast<ncclComm_t>(comm), (hipStream_t)stream);
+    HIPCHK(hipSetDevice(prev));
+    if (r != ncclSuccess) return fail(PGMI_E_HIP, std::string("ncclBroadcast: ") + rccl().error_string(r));
     x->prepared = false;  // derived tensors are rebuilt from the received weights by pgmi_prepare
     return 0;
 }
@@ -1131,26 +1208,13 @@ int pgmi_tune_gemm(int cfg, int split) {
     return 0;
 }
 
-int pgmi_debug_stamps(int which, long long* host, long n_words) {
-    if (!host || n_words < 0) return fail(PGMI_E_ARG, "bad argument");
-    if (which != 0) return fail(PGMI_E_ARG, "unknown stamp buffer");
-    if (attn_debug_stamps(host, n_words)) return fail(PGMI_E_HIP, "stamp read-back failed");
-    return 0;
-}
-
 int pgmi_tune_attention(int variant) {
-    static const int ok[] = {-1, 0, 8, 9, 41, 42, 21, 22, 44, 24, 91, 92, 94};
+    static const int ok[] = {-1, 0, 8, 41, 42, 21, 22, 44, 24};
     for (int v : ok)
         if (v == variant) {
             attention_force_variant(variant);
             return 0;
         }
-    // tiled kernel with a register prefetch of PD = 2..4 tiles: 100 * PD + (41, 42, 21, 22, 44, 24)
-    const int pd = variant / 100, rk = variant % 100;
-    if (pd >= 2 && pd <= 4 && (rk == 41 || rk == 42 || rk == 21 || rk == 22 || rk == 44 || rk == 24)) {
-        attention_force_variant(variant);
-        return 0;
-    }
     return fail(PGMI_E_ARG, "unknown attention variant");
 }
 

@@ -65,13 +65,6 @@ __device__ __forceinline__ void attn_out_rows(const AttnArgs& a, int b, int kvh,
     }
 }
 
-__device__ long long g_attn_stamps[kStampWords];  // diagnostic stamps of the STAMP kernel variants
-
-int attn_debug_stamps(long long* host, long n_words) {
-    const long n = n_words < kStampWords ? n_words : kStampWords;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -1;
-}
-
 template <int HD>
 __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
     using I = HDInfo<HD>;
@@ -222,7 +215,7 @@ __global__ void __launch_bounds__(256) k_attn_full(AttnArgs a) {
 // their chunk is staged) -- so the kernel pays one L2 round trip instead of one per K tile and per
 // V chunk.  Keys <= 16 * 4 * MAXT and <= 32 * MAXC.  Scores are kept in LDS as bf16 (they are
 // bf16-rounded values, modeling_gemma.py:266) and P overwrites them row by row.
-template <int HD, int MAXT, int MAXC, bool STAMP = false>
+template <int HD, int MAXT, int MAXC>
 __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     using I = HDInfo<HD>;
     constexpr int HDP = I::CT * 16;
@@ -245,8 +238,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
     const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
     const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
     const int ntile = LkP / 16, nch = LkP / CHK;
-    const int slot = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 0);
 
     short8 qf[I::KS];
 #pragma unroll
@@ -271,7 +262,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
             const int key = c * CHK + e / I::CH, ch = e % I::CH;
             vr[c][i] = ldg16(vbase + (long)(key < a.Lk ? key : a.Lk - 1) * a.v_row_stride + ch * 8);  // p = 0 past Lk
         }
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 1);
 
     // ---- phase 1: s = bf16(bf16(Q K^T) * scale), kept in registers: lane (g, li) holds rows 4g + r
     // of keys 16 t + li for this wave's tiles t = wave + 4 j
@@ -287,7 +277,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) sc[j][r] = (t < ntile && key < a.Lk) ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
     }
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 2);
     // ---- phase 2: exact softmax per row: max and sum of exp over the row's keys (lane, then the 16
     // lanes of a row group, then the 4 waves in a fixed order), p = bf16(exp(s - max) / sum) -> LDS
     float* red = reinterpret_cast<float*>(Vl + 2 * CHK * VS);  // [2][4 waves][16 rows]
@@ -337,7 +326,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
             if (key < LkP) S[row * LkP + key] = key < a.Lk ? f2bf(sc[j][r] / L) : 0;
         }
     }
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 3);
     // ---- phase 3: O = bf16(P V), V chunks staged from registers into two LDS buffers
     f32x4 oacc[(I::CT + 3) / 4];
 #pragma unroll
@@ -372,7 +360,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         }
         }
     }
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 4);
     uint16_t* orow[4];
     attn_out_rows(a, b, kvh, row0 + (lane >> 4) * 4, nrows, orow);
 #pragma unroll
@@ -385,7 +372,6 @@ __global__ void __launch_bounds__(256) k_attn_full_pre(AttnArgs a) {
         for (int r = 0; r < 4; ++r)
             if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
     }
-    if constexpr (STAMP) stamp_to(g_attn_stamps, slot, 5);
 }
 
 // ---------------------------------------------------------------- prefill, K/V-tiled (two pass)
@@ -655,232 +641,40 @@ __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
     }
 }
 
-// ---------------------------------------------------------------- prefill, K/V resident in LDS
-// Short key ranges (SigLIP at 224 px: 256 keys x d 72): the workgroup copies ALL keys and values of
-// its (b, kv head) into LDS in one round trip (every load issued before the first wait), then each
-// wave runs k_attn_fa's two passes over its 16 query rows from LDS with no further barrier: no
-// per-tile global round trips, which bound the tiled kernel at this size.  Same rounding points
-// and the same lane layout as k_attn_fa (transposed scores S^T = K Q^T, so a lane's 8 scores of a
-// 32-key tile are the A fragment of P for the P.V MFMA).
-template <int HD>
-constexpr size_t attn_lds_bytes(int Lk) {
-    return (size_t)((Lk + 31) & ~31) * (FAInfo<HD>::KRS + FAInfo<HD>::VS) * 2;
-}
-
-template <int HD, int W>
-__global__ void __launch_bounds__(64 * W) k_attn_lds(AttnArgs a) {
-    using I = FAInfo<HD>;
-    constexpr int KS = I::KS, CT = I::CT, CH = I::CH, KRC = I::KRC, KRS = I::KRS, VS = I::VS;
-    constexpr int NT = 64 * W;
-    extern __shared__ __attribute__((aligned(16))) uint16_t lsm[];
-    const int LkP = (a.Lk + 31) & ~31;
-    uint16_t* Kl = lsm;                 // [LkP][KRS], 16-B chunk c of row r at chunk c ^ (r & 15)
-    uint16_t* Vl = lsm + LkP * KRS;     // [LkP][VS]
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    const int b = blockIdx.z, kvh = blockIdx.y;
-    const int nrows = a.Lq * a.G;
-    const int qi = blockIdx.x * (16 * W) + wave * 16 + li;
-    const bool qvalid = qi < nrows;
-    const int qpos = qvalid ? qi / a.G : 0, qhead = kvh * a.G + (qvalid ? qi % a.G : 0);
-    const uint16_t* qrow = a.q + b * a.q_b_stride + (long)qpos * a.q_row_stride + qhead * a.q_head_stride;
-    const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
-    const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
-
-    // ---- stage K and V: up to 10 16-B loads per thread and tensor in flight per round (one round
-    // for SigLIP-224 at 4 waves); rows past Lk and chunks past HD are zero
-    constexpr int RPT = (NT * 10 / CH) / 32 * 32 > 0 ? (NT * 10 / CH) / 32 * 32 : 32;  // rows per round
-    constexpr int LPT = (RPT * CH + NT - 1) / NT;
-    for (int r0 = 0; r0 < a.Lk; r0 += RPT) {
-        uint4 kr[LPT], vr[LPT];
-#pragma unroll
-        for (int i = 0; i < LPT; ++i) {
-            const int e = tid + NT * i, r = r0 + e / CH, c = e % CH;
-            const bool ok = e < RPT * CH && r < a.Lk;
-            kr[i] = ldg16_sel(kbase + (long)r * a.k_row_stride + c * 8, ok, kbase);
-            vr[i] = ldg16_sel(vbase + (long)r * a.v_row_stride + c * 8, ok, vbase);
-        }
-#pragma unroll
-        for (int i = 0; i < LPT; ++i) {
-            const int e = tid + NT * i, r = r0 + e / CH, c = e % CH;
-            if (e < RPT * CH && r < LkP) {
-                *reinterpret_cast<uint4*>(Kl + r * KRS + ((c ^ (r & 15)) << 3)) = kr[i];
-                *reinterpret_cast<uint4*>(Vl + r * VS + c * 8) = vr[i];
-            }
-        }
-    }
-    // zero: K pad chunks (k-steps past HD read them), V columns HD..16*CT (the last P.V tile), and
-    // the rows Lk..LkP of both
-    constexpr int VZ = CT * 2 - CH;  // 16-B V chunks past HD inside the last 16-column tile
-    if constexpr (KRC > CH) {
-        for (int e = tid; e < LkP * (KRC - CH); e += NT) {
-            const int r = e / (KRC - CH), c = CH + e % (KRC - CH);
-            *reinterpret_cast<uint4*>(Kl + r * KRS + ((c ^ (r & 15)) << 3)) = make_uint4(0, 0, 0, 0);
-        }
-    }
-    if constexpr (VZ > 0) {
-        for (int e = tid; e < LkP * VZ; e += NT)
-            *reinterpret_cast<uint4*>(Vl + (e / VZ) * VS + (CH + e % VZ) * 8) = make_uint4(0, 0, 0, 0);
-    }
-    for (int e = tid; e < (LkP - a.Lk) * KRC; e += NT) {
-        const int r = a.Lk + e / KRC, c = e % KRC;
-        *reinterpret_cast<uint4*>(Kl + r * KRS + (c << 3)) = make_uint4(0, 0, 0, 0);
-        if (c < CT * 2) *reinterpret_cast<uint4*>(Vl + r * VS + c * 8) = make_uint4(0, 0, 0, 0);
-    }
-    short8 qf[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) qf[kk] = load_frag<HD>(qrow, qvalid, kk, lane);
-    __syncthreads();
-
-    auto scores = [&](int t, float (&s)[2][4]) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-            const int r = t * 32 + kt * 16 + li;
-            const uint16_t* kp = Kl + r * KRS;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                const short8 kf = *reinterpret_cast<const short8*>(kp + (((kk * 4 + g) ^ (r & 15)) << 3));
-                acc = mfma16(kf, qf[kk], acc);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = t * 32 + kt * 16 + 4 * g + j;
-                s[kt][j] = key < a.Lk ? rbf(rbf(acc[j]) * a.scale) : -INFINITY;
-            }
-        }
-    };
-    const int nt = LkP / 32;
-    // ---- pass 1: per-row max and sum of exp (lane-local online, then the 4 lane groups)
-    float m = -INFINITY, l = 0.f;
-    for (int t = 0; t < nt; ++t) {
-        float s[2][4];
-        scores(t, s);
-        float tm = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) tm = fmaxf(tm, s[kt][j]);
-        const float mn = fmaxf(m, tm);
-        if (mn != -INFINITY) {
-            float ts = 0.f;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) ts += fa_exp(s[kt][j] - mn);
-            l = (m == -INFINITY ? 0.f : l * fa_exp(m - mn)) + ts;
-            m = mn;
-        }
-    }
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-        const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
-        if (lane & o) fa_comb(m, l, m2, l2);
-        else {
-            float mm = m2, ll = l2;
-            fa_comb(mm, ll, m, l);
-            m = mm;
-            l = ll;
-        }
-    }
-    const float invl = 1.0f / l;
-    // ---- pass 2: O = sum over tiles of bf16(p) . V
-    f32x4 oacc[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nt; ++t) {
-        float s[2][4];
-        scores(t, s);
-        short8 pa;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pa[kt * 4 + j] = (short)f2bf(fa_exp(s[kt][j] - m) * invl);
-        const uint16_t* vb0 = Vl + (t * 32 + 4 * g + (li >> 2)) * VS + 4 * (li & 3);
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vb0 + c * 16));
-            const s4v hi =
-                __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vb0 + 16 * VS + c * 16));
-            const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            oacc[c] = mfma16(pa, vb, oacc[c]);
-        }
-    }
-    uint16_t* orow[4];
-    attn_out_rows(a, b, kvh, blockIdx.x * (16 * W) + wave * 16 + 4 * g, nrows, orow);
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-        const int d = c * 16 + li;
-        if (d >= HD) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
-    }
-}
-
-template <int HD, int W>
-static void launch_attn_lds(hipStream_t s, const AttnArgs& a) {
-    const size_t lds = attn_lds_bytes<HD>(a.Lk);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_lds<HD, W>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
-    dim3 grid((a.Lq * a.G + 16 * W - 1) / (16 * W), a.n_kv, a.B);
-    hipLaunchKernelGGL((k_attn_lds<HD, W>), grid, dim3(64 * W), lds, s, a);
-}
-
-template <int HD, int RG, int KSPL, int PD = 1>
+template <int HD, int RG, int KSPL>
 static void launch_fa(hipStream_t s, const AttnArgs& a) {
     using I = FAInfo<HD>;
     constexpr size_t lds = (size_t)KSPL * 2 * 32 * (I::KRS + I::VS) * 2 + (size_t)KSPL * RG * 16 * 2 * 4;
     static_assert(lds <= 160 * 1024, "LDS");
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fa<HD, RG, KSPL, PD>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fa<HD, RG, KSPL, 1>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     dim3 grid((a.Lq * a.G + 16 * RG - 1) / (16 * RG), a.n_kv, a.B);
-    hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL, PD>), grid, dim3(64 * RG * KSPL), lds, s, a);
+    hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL, 1>), grid, dim3(64 * RG * KSPL), lds, s, a);
 }
 
-// attention variant override (tuning hook pgmi_tune_attention / env PGMI_ATTN): 0 = the 16-row
-// kernel, RK = the tiled kernel with RG = R, KSPL = K (41, 42, 21, 22; 44 and 24 for HD 72);
-// -1 = the measured choice in attention_prefill
-static int g_attn_force = [] {
-    const char* e = std::getenv("PGMI_ATTN");
-    return e ? std::atoi(e) : -1;
-}();
+// attention variant override (tuning hook pgmi_tune_attention): 0 = the 16-row kernel, 8 = the
+// 16-row kernel with every load up front (HD 256, <= 320 keys), RK = the tiled kernel with RG = R,
+// KSPL = K (41, 42, 21, 22; 44 and 24 for HD 72); -1 = the measured choice in attention_prefill.
+// Every variant is forced and checked against the oracle by tests/test_gpu_ops.py.
+static int g_attn_force = -1;
 
 void attention_force_variant(int v) { g_attn_force = v; }
 
-// variant = 100 * PD + 10 * RG + KSPL (PD = register prefetch depth in tiles; < 100: PD 1)
-template <int HD, int PD>
-static bool launch_fa_pd(hipStream_t s, const AttnArgs& a, int rk) {
+template <int HD>
+static void launch_fa_variant(hipStream_t s, const AttnArgs& a, int rk) {
     switch (rk) {
-        case 41: launch_fa<HD, 4, 1, PD>(s, a); return true;
-        case 42: launch_fa<HD, 4, 2, PD>(s, a); return true;
-        case 21: launch_fa<HD, 2, 1, PD>(s, a); return true;
-        case 22: launch_fa<HD, 2, 2, PD>(s, a); return true;
-        case 44: if constexpr (HD == 72) { launch_fa<HD, 4, 4, PD>(s, a); return true; } break;
-        case 24: if constexpr (HD == 72) { launch_fa<HD, 2, 4, PD>(s, a); return true; } break;
+        case 41: launch_fa<HD, 4, 1>(s, a); return;
+        case 21: launch_fa<HD, 2, 1>(s, a); return;
+        case 22: launch_fa<HD, 2, 2>(s, a); return;
+        case 44: if constexpr (HD == 72) { launch_fa<HD, 4, 4>(s, a); return; } break;
+        case 24: if constexpr (HD == 72) { launch_fa<HD, 2, 4>(s, a); return; } break;
         default: break;
     }
-    return false;
-}
-
-template <int HD>
-static void launch_fa_variant(hipStream_t s, const AttnArgs& a, int v) {
-    const int pd = v / 100, rk = v % 100;
-    bool ok = false;
-    if (pd <= 1) ok = launch_fa_pd<HD, 1>(s, a, rk);
-    else if (pd == 2) ok = launch_fa_pd<HD, 2>(s, a, rk);
-    else if (pd == 3) ok = launch_fa_pd<HD, 3>(s, a, rk);
-    else ok = launch_fa_pd<HD, 4>(s, a, rk);
-    if (!ok) launch_fa<HD, 4, 2, 1>(s, a);
+    launch_fa<HD, 4, 2>(s, a);  // 42
 }
 
 static size_t attn_full_lds(int head_dim, int Lk) {
@@ -891,23 +685,6 @@ static size_t attn_full_lds(int head_dim, int Lk) {
 
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
     int v = g_attn_force;
-    // K/V-resident kernel (variants 91, 92, 94: 1, 2, 4 waves of 16 query rows per workgroup)
-    const bool lds_fits = head_dim == 72 ? attn_lds_bytes<72>(a.Lk) <= 160 * 1024
-                                         : attn_lds_bytes<256>(a.Lk) <= 160 * 1024;
-    // (opt-in only: at SigLIP 224 variant 94 measured 15.7 us against 10.7 for RG2xKSPL4)
-    if (v >= 91 && v <= 94 && lds_fits) {
-        if (head_dim == 72) {
-            if (v == 91) launch_attn_lds<72, 1>(s, a);
-            else if (v == 94) launch_attn_lds<72, 4>(s, a);
-            else launch_attn_lds<72, 2>(s, a);
-        } else {
-            if (v == 91) launch_attn_lds<256, 1>(s, a);
-            else if (v == 94) launch_attn_lds<256, 4>(s, a);
-            else launch_attn_lds<256, 2>(s, a);
-        }
-        return;
-    }
-    if (v >= 91 && v < 100) v = -1;
     if (v < 0) {
         // measured on MI355X (tools/probes/attn_bench.py, round 1), us per call:
         //   SigLIP 224 (256 rows x 16 heads):  16-row 16.4 | RG2xKSPL4 10.8 | RG4xKSPL2 13.5
@@ -919,15 +696,14 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         if (head_dim == 256) v = rows <= 4096 ? (a.Lk <= 320 ? 8 : 0) : 42;
         else v = rows <= 8192 ? 24 : 44;
     }
-    if ((v == 8 || v == 9) && head_dim == 256 && a.Lk <= 320) {
+    if (v == 8 && head_dim == 256 && a.Lk <= 320) {
         // 16 query rows per workgroup, every K/V load issued up front (Lk <= 320)
         const size_t lds = (size_t)16 * ((a.Lk + 31) & ~31) * 2 + (size_t)2 * 32 * (256 + 16) * 2 + 2 * 4 * 16 * 4;
         dim3 grid((a.Lq * a.G + 15) / 16, a.n_kv, a.B);
-        if (v == 9) hipLaunchKernelGGL((k_attn_full_pre<256, 5, 10, true>), grid, dim3(256), lds, s, a);  // stamped
-        else hipLaunchKernelGGL((k_attn_full_pre<256, 5, 10>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_attn_full_pre<256, 5, 10>), grid, dim3(256), lds, s, a);
         return;
     }
-    if (v == 8 || v == 9) v = 0;
+    if (v == 8) v = 0;
     if (v != 0 || a.Lk > attention_prefill_max_keys(head_dim)) {
         if (head_dim == 256) launch_fa_variant<256>(s, a, v);
         else launch_fa_variant<72>(s, a, v);

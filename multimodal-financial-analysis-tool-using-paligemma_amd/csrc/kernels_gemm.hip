@@ -402,7 +402,7 @@ template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                    int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
-                                                   int n_mt, int n_nt, int krot) {
+                                                   int n_mt, int n_nt) {
     constexpr int WN = NW / WM;
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
@@ -436,9 +436,6 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     int kt1 = kt0 + kt_per_split;
     if (kt1 > nkt_total) kt1 = nkt_total;
     const int nkt = kt1 - kt0;
-    // k-tile order rotated per column tile: workgroups sharing A rows start at different k, so
-    // they do not all hit the same L2 lines (channels) at once
-    const int rot = nkt > 0 ? (nt * krot) % nkt : 0;
 
     // per-lane source rows of this wave's pieces (piece p = wave + NW i)
     const uint16_t* src[GPW];
@@ -476,8 +473,6 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #define PGMI_LDS_AT(slot, i) ((__attribute__((address_space(3))) void*)(smem_p + (slot) * SBYTES + loff[i]))
     const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
     auto issue = [&](int kt, int slot) {
-        kt += rot;
-        if (kt >= kt1) kt -= nkt;
         const int kel = kt * 64;
         if (kel + 64 <= K) {
 #pragma unroll
@@ -861,10 +856,6 @@ struct Plan {
 };
 
 static int g_force_cfg = -1, g_force_split = 0;  // tuning override (pgmi_tune_gemm)
-static int g_krot = [] {  // panel GEMM k-order rotation per column tile (PGMI_GEMM_KROT; 0 = off)
-    const char* v = std::getenv("PGMI_GEMM_KROT");
-    return v ? std::atoi(v) : 0;
-}();
 
 void gemm_force_plan(int cfg, int split) {
     g_force_cfg = cfg;
@@ -922,7 +913,7 @@ static Plan choose(int M, int N, int K, bool dual) {
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
-    // lock-step decode batches as GEMMs (M <= 16 rows, PGMI_DEC_MLP_GEMM; tools/gemm_sweep.py b8_*
+    // lock-step decode batches as GEMMs (M <= 16 rows; tools/gemm_sweep.py b8_*
     // in isolation: gate|up 64x128 tiles 24.2 us, down 64x64 split 8 18.1 us)
     if (M <= 16) {
         if (dual) return mk(P64x128, 1);
@@ -1009,7 +1000,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
     if (EPI < 0 || split > 1) {
         hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
-                           ea, ws, up_off, n_mt, n_nt, g_krot);
+                           ea, ws, up_off, n_mt, n_nt);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1018,7 +1009,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         }
     } else {
         hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, n_mt, n_nt, g_krot);
+                           per, ea, ws, up_off, n_mt, n_nt);
     }
 }
 
@@ -1152,11 +1143,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
 
 bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                    const EpiArgs& ea) {
-    static const bool off = [] {
-        const char* v = std::getenv("PGMI_QKV_ROPE");
-        return v && v[0] == '0';
-    }();
-    if (off || N % 256 != 0 || N != (ea.nh + 2 * ea.nkv) * 256) return false;
+    if (N % 256 != 0 || N != (ea.nh + 2 * ea.nkv) * 256) return false;
     const Plan p = choose(M, N, K, false);
     if (p.split != 1) return false;
     // configurations with two 16-column tiles per wave and a tile width dividing 256

@@ -1,8 +1,6 @@
 // kernels_gemv.hip -- launchers of the decode GEMV kernels (bodies: gemv_body.h).
 #include "gemv_body.h"
 
-#include <cstdlib>
-
 namespace pgmi {
 
 // MFMA path for 3..16 lock-step sequences (kernels_gemv_mfma.hip)
@@ -12,12 +10,6 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a);
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o);
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks);
 void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws);
-
-// launch-shape overrides for measurement sweeps (tools/gemv_sweep.py)
-static int tune_variant(const char* env, int dflt) {
-    const char* v = std::getenv(env);
-    return v ? std::atoi(v) : dflt;
-}
 
 template <int B, int KCH, int RPW, int MODE, int WK = 1, int DEPTH = 1, bool EMB = false>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
@@ -47,8 +39,7 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;
     if (emb) {  // layer 0: the token's embedding row is the input (and is written to h)
         a.ids = emb->ids; a.E = emb->E; a.normalizer = emb->normalizer; a.pad_id = emb->pad_id; a.emb_out = emb->h_out;
-        const int cap = tune_variant("PGMI_QKV_CAP", 0);
-        if (B <= 1) launch_gemv<1, 4, 1, GV_QKV, 1, 1, true>(s, a, cap);
+        if (B <= 1) launch_gemv<1, 4, 1, GV_QKV, 1, 1, true>(s, a);
         else launch_gemv<2, 4, 1, GV_QKV, 1, 1, true>(s, a);
         return;
     }
@@ -57,14 +48,8 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
         gemv_mf_qkv(s, a, ws);
         return;
     }
-    if (B <= 1) {
-        const int cap = tune_variant("PGMI_QKV_CAP", 0);
-        if (tune_variant("PGMI_QKV_RPW", 1) == 2) launch_gemv<1, 4, 2, GV_QKV>(s, a, cap);
-        else launch_gemv<1, 4, 1, GV_QKV>(s, a, cap);
-    }
-    else if (B <= 2) L_(2, 4, 1, GV_QKV);
-    else if (B <= 4) L_(4, 4, 1, GV_QKV);
-    else L_(8, 4, 1, GV_QKV);
+    if (B <= 1) L_(1, 4, 1, GV_QKV);
+    else L_(2, 4, 1, GV_QKV);  // B >= 3 runs on MFMA (above)
 }
 
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
@@ -85,16 +70,8 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
             const int nb = (B - b0) < 4 ? (B - b0) : 4;
             GemvArgs c = a;
             c.x = x + (long)b0 * K; c.out = h_inout + (long)b0 * N; c.nb = nb;
-            if (nb <= 1) {
-                const int cap = tune_variant("PGMI_DOWN_CAP", 512);
-                const int rpw = tune_variant("PGMI_DOWN_RPW", 1);
-                const int wk = tune_variant("PGMI_DOWN_WK", 4);
-                if (tune_variant("PGMI_DOWN_DEPTH", 1) == 2) launch_gemv<1, 32, 1, GV_RES, 4, 2>(s, c, cap);
-                else if (wk == 2) launch_gemv<1, 32, 1, GV_RES, 2>(s, c, cap);
-                else if (wk == 1) launch_gemv<1, 32, 1, GV_RES, 1>(s, c, cap);
-                else if (rpw == 1) launch_gemv<1, 32, 1, GV_RES, 4>(s, c, cap);
-                else launch_gemv<1, 32, 2, GV_RES, 4>(s, c, cap);
-            }
+            // K split in 4 inside the workgroup: 512 workgroups of one row each
+            if (nb <= 1) launch_gemv<1, 32, 1, GV_RES, 4>(s, c, 512);
             else if (nb <= 2) launch_gemv<2, 32, 2, GV_RES, 4>(s, c);
             else launch_gemv<4, 32, 2, GV_RES, 4>(s, c);
         }
@@ -111,11 +88,7 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
         return;
     }
     // grid capped so each workgroup's combine prologue is amortised over 8 output rows
-    if (B <= 1) {
-        const int cap = tune_variant("PGMI_O_CAP", 256);
-        if (tune_variant("PGMI_O_RPW", 2) == 1) launch_gemv<1, 4, 1, GV_ORES>(s, a, cap);
-        else launch_gemv<1, 4, 2, GV_ORES>(s, a, cap);
-    }
+    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 2) launch_gemv<2, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 4) launch_gemv<4, 4, 1, GV_ORES>(s, a, 256);
     else launch_gemv<8, 4, 1, GV_ORES>(s, a, 256);
@@ -129,25 +102,14 @@ void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w,
         gemv_mf_geglu(s, a);
         return;
     }
-    if (B <= 1) {
-        const int cap = tune_variant("PGMI_GU_CAP", 1024);
-        const int rpw = tune_variant("PGMI_GU_RPW", 1);
-        if (tune_variant("PGMI_GU_DEPTH", 1) == 2) launch_gemv<1, 4, 1, GV_GEGLU, 1, 2>(s, a, cap);
-        else if (rpw == 1) launch_gemv<1, 4, 1, GV_GEGLU>(s, a, cap);
-        else launch_gemv<1, 4, 2, GV_GEGLU>(s, a, cap);
-    }
-    else if (B <= 2) L_(2, 4, 2, GV_GEGLU);
-    else if (B <= 4) L_(4, 4, 2, GV_GEGLU);
-    else L_(8, 4, 1, GV_GEGLU);
+    if (B <= 1) launch_gemv<1, 4, 1, GV_GEGLU>(s, a, 1024);
+    else L_(2, 4, 2, GV_GEGLU);  // B >= 3 runs on MFMA (above)
 }
 
 int gemv_logits_blocks() { return 2048; }
 
 // the streaming lm_head (B < the MFMA batch) folds the argmax into its last workgroup
-bool gemv_logits_folds(int B) {
-    static const int on = tune_variant("PGMI_LM_FOLD", 1);
-    return on != 0 && B < gemv_mf_min_batch();
-}
+bool gemv_logits_folds(int B) { return B < gemv_mf_min_batch(); }
 
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
                  int V, float* logits, float* pmax, int* pidx, int* nparts, unsigned* done, int64_t* next,
@@ -155,8 +117,7 @@ bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
-    int mb = tune_variant("PGMI_LM_CAP", gemv_logits_blocks());
-    if (mb < 1 || mb > gemv_logits_blocks()) mb = gemv_logits_blocks();  // pmax/pidx capacity
+    const int mb = gemv_logits_blocks();  // pmax/pidx capacity
     int blocks;
     if (B >= gemv_mf_min_batch()) {
         *nparts = gemv_mf_logits(s, a, mb);
@@ -174,20 +135,8 @@ bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
         if (blocks > mb) blocks = mb;                                   \
         launch_gemv<b_, 4, rpw, GV_LOGITS>(s, a, mb);                   \
     } while (0)
-    if (B <= 1) {
-        if (tune_variant("PGMI_LM_DEPTH", 1) == 2) {
-            blocks = (V + 8 - 1) / 8;
-            if (blocks > mb) blocks = mb;
-            launch_gemv<1, 4, 2, GV_LOGITS, 1, 2>(s, a, mb);
-        } else if (tune_variant("PGMI_LM_RPW", 4) == 2) {
-            LG_(1, 2);
-        } else {
-            LG_(1, 4);
-        }
-    }
-    else if (B <= 2) LG_(2, 4);
-    else if (B <= 4) LG_(4, 2);
-    else LG_(8, 2);
+    if (B <= 1) LG_(1, 4);
+    else LG_(2, 4);  // B >= 3 runs on MFMA (above)
     *nparts = blocks;
     return fold;
 #undef LG_

@@ -19,8 +19,6 @@
 //     fp32 logits + per-workgroup first-max argmax partials).
 #include "gemv_body.h"
 
-#include <cstdlib>
-
 namespace pgmi {
 
 constexpr int MF_MAXB = 16;
@@ -132,13 +130,12 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     const int k0 = (ks * WK + wk) * KW;
     const int n_groups = (a.n_units + 15) / 16;
 
-    // GV_QKV, NR 2: unit u = rotary pair (d, d + 128) of head u >> 7 in one lane (two row sets).
-    // GV_QKV, NR 1: unit u = one weight row; a 16-row group is 8 rotary pairs of one head, d in lanes
+    // GV_QKV: unit u = one weight row; a 16-row group is 8 rotary pairs of one head, d in lanes
     // n < 8 and d + 128 in lane n + 8 (the partner value is one lane swap away in the C map), so the
-    // 2,560 rows make 160 groups (twice the workgroups of the pair form)
+    // 2,560 rows make 160 groups
+    static_assert(MODE != GV_QKV || NR == 1, "q|k|v: one weight row per lane");
     auto row_of = [&](int u, int j) -> long {
-        if constexpr (MODE == GV_QKV && NR == 2) return (long)((u >> 7) * 256 + (u & 127) + j * 128);
-        else if constexpr (MODE == GV_QKV) {
+        if constexpr (MODE == GV_QKV) {
             const int grp_ = u >> 4, nn = u & 15;
             return (long)((grp_ >> 4) * 256 + (grp_ & 15) * 8 + (nn & 7) + (nn >> 3) * 128);
         }
@@ -166,7 +163,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     if constexpr (MODE == GV_QKV) {
         int p0 = a.st->position;
         p0 = p0 < 0 ? 0 : (p0 > a.max_pos - 1 ? a.max_pos - 1 : p0);
-        const int d0 = NR == 2 ? ((grp * 16 + n) & 127) : ((grp & 15) * 8 + (n & 7));
+        const int d0 = (grp & 15) * 8 + (n & 7);
         cs0 = bf2f(a.cosT[(long)p0 * 128 + d0]);
         sn0 = bf2f(a.sinT[(long)p0 * 128 + d0]);
     }
@@ -234,7 +231,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
         }
         // C map: col n = unit (cur*16 + n), row b = 4g + r
         const int u = cur * 16 + n;
-        if constexpr (MODE == GV_QKV && NR == 1) {
+        if constexpr (MODE == GV_QKV) {
             // the rotary partner of this lane's row is lane n ^ 8's (same rows b)
             f32x4 part;
 #pragma unroll
@@ -277,24 +274,6 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 const float v = rbf(acc[0][r]);
                 a.logits[(long)b * a.n_units + u] = v;
                 if (v > best[r]) { best[r] = v; besti[r] = u; }  // units visited in increasing order
-            } else {  // GV_QKV
-                const int hh = u >> 7, d = u & 127;
-                const float x0 = rbf(acc[0][r]), x1 = rbf(acc[1][r]);
-                const int nh = a.I;
-                if (hh < nh + a.nkv) {
-                    const float c = cur == grp0 ? cs0 : bf2f(a.cosT[(long)pos * 128 + d]);
-                    const float sn = cur == grp0 ? sn0 : bf2f(a.sinT[(long)pos * 128 + d]);
-                    const uint16_t o0 = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
-                    const uint16_t o1 = f2bf(rbf(x1 * c) + rbf(x0 * sn));
-                    uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256
-                                            : a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
-                    dst[d] = o0;
-                    dst[d + 128] = o1;
-                } else {
-                    uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh - a.nkv) * 256;
-                    dst[d] = f2bf(x0);
-                    dst[d + 128] = f2bf(x1);
-                }
             }
         }
     }
@@ -320,140 +299,6 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
         if (tid < a.nb) {
             a.pmax[(long)tid * gridDim.x + blockIdx.x] = bv[tid];
             a.pidx[(long)tid * gridDim.x + blockIdx.x] = bi[tid];
-        }
-    }
-}
-
-// ---------------------------------------------------------------- streaming form
-// One wave streams whole 16-row groups over a KSL-wide K slice with D 128-wide k blocks in
-// flight (the B=1 GEMV's access pattern, MFMA instead of v_dot2), groups dealt grid-stride to
-// the 4 waves of each workgroup; the workgroup stages its K slice of the activation rows in LDS
-// once (RMSNorm fused when the slice is the whole row) and every MFMA reads its A fragment
-// there.  grid.y = K slices (GV_RES only: fp32 partials to ws, reduced by k_mf_combine).
-template <int MODE, int NR, int KSL, int D>
-__global__ void __launch_bounds__(256) k_gemv_ms(GemvArgs a, float* __restrict__ ws) {
-    constexpr int NKB = KSL / 128;
-    static_assert(NKB % D == 0, "k blocks per slice must be a multiple of the pipeline depth");
-    extern __shared__ __attribute__((aligned(16))) uint16_t mss[];
-    __shared__ float red[MF_MAXB * 16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = lane & 15, g = lane >> 4;
-    const int K = a.K, ld = KSL + 8;
-    const int KS = gridDim.y, ks = blockIdx.y;
-    const int k0 = ks * KSL;
-    const int n_groups = (a.n_units + 15) / 16;
-    const int gstride = gridDim.x * 4;
-
-    auto row_of = [&](int u, int j) -> long {
-        if constexpr (MODE == GV_GEGLU) return (long)u + (long)j * a.I;
-        else return (long)u;
-    };
-    uint4 w[D][NR][4];
-    auto rot_of = [&](int grp) { return grp % NKB; };  // k-block order rotated per group (see k_gemv_ml)
-    auto issue = [&](int grp, int kb, int slot) {
-        kb += rot_of(grp);
-        if (kb >= NKB) kb -= NKB;
-        int u = grp * 16 + n;
-        if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const uint16_t* rp = a.W + row_of(u, j) * K + k0 + kb * 128 + 8 * g;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) w[slot][j][i] = ldg16(rp + 32 * i);
-        }
-    };
-    int grp = blockIdx.x * 4 + wave;
-    if (grp < n_groups) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) issue(grp, d, d);
-    }
-    // stage x[:, k0 : k0 + KSL] (rows < nb) in LDS; the whole row carries the RMSNorm
-    if (a.norm_w) {
-        mf_stage_rows(a, K, mss, ld, red);
-    } else {
-        for (int c = tid * 8; c < KSL; c += 256 * 8) {  // all rows' chunks in one round trip
-            uint4 v[MF_MAXB];
-#pragma unroll
-            for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): one round trip
-                v[b] = ldg16(a.x + (long)(b < a.nb ? b : a.nb - 1) * K + k0 + c);
-#pragma unroll
-            for (int b = 0; b < MF_MAXB; ++b)
-                if (b < a.nb) *reinterpret_cast<uint4*>(mss + b * ld + c) = v[b];
-        }
-    }
-    __syncthreads();
-    const int xrow = n < a.nb ? n : 0;  // rows >= nb: read row 0, zeroed below
-    const uint16_t* xa = mss + xrow * ld + 8 * g;
-    const bool xz = n >= a.nb;
-
-    float best[4];
-    int besti[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { best[r] = -INFINITY; besti[r] = 0x7fffffff; }
-
-    for (; grp < n_groups; grp += gstride) {
-        const int nxt = grp + gstride;
-        const int rot = rot_of(grp);
-        f32x4 acc[NR];
-#pragma unroll
-        for (int j = 0; j < NR; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-            const int slot = kb % D;
-            const int kr = kb + rot < NKB ? kb + rot : kb + rot - NKB;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                short8 xv = *reinterpret_cast<const short8*>(xa + kr * 128 + 32 * i);
-                if (xz) xv = short8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-                for (int j = 0; j < NR; ++j) acc[j] = mfma16(xv, __builtin_bit_cast(short8, w[slot][j][i]), acc[j]);
-            }
-            // refill the slot: block kb + D of this group, or the head of the next group
-            if (kb + D < NKB) issue(grp, kb + D, slot);
-            else if (nxt < n_groups) issue(nxt, kb + D - NKB, slot);
-        }
-        const int u = grp * 16 + n;
-        if (u >= a.n_units) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int b = 4 * g + r;
-            if (b >= a.nb) break;
-            if constexpr (MODE == GV_RES) {
-                if (KS > 1) ws[((long)ks * a.nb + b) * a.n_units + u] = acc[0][r];
-                else a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
-            } else if constexpr (MODE == GV_GEGLU) {
-                const float gg = rbf(gelu_tanh(rbf(acc[0][r])));
-                a.out[(long)b * a.I + u] = f2bf(gg * rbf(acc[1][r]));
-            } else {  // GV_LOGITS
-                const float v = rbf(acc[0][r]);
-                a.logits[(long)b * a.n_units + u] = v;
-                if (v > best[r]) { best[r] = v; besti[r] = u; }  // units visited in increasing order
-            }
-        }
-    }
-    if constexpr (MODE == GV_LOGITS) {
-        __shared__ float bv[4][MF_MAXB];
-        __shared__ int bi[4][MF_MAXB];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float m = best[r];
-            int mi = besti[r];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const float m2 = __shfl_xor(m, o, 64);
-                const int i2 = __shfl_xor(mi, o, 64);
-                if (m2 > m || (m2 == m && i2 < mi)) { m = m2; mi = i2; }
-            }
-            if (n == 0) { bv[wave][4 * g + r] = m; bi[wave][4 * g + r] = mi; }
-        }
-        __syncthreads();
-        if (tid < a.nb) {
-            float m = bv[0][tid];
-            int mi = bi[0][tid];
-            for (int q = 1; q < 4; ++q)
-                if (bv[q][tid] > m || (bv[q][tid] == m && bi[q][tid] < mi)) { m = bv[q][tid]; mi = bi[q][tid]; }
-            a.pmax[(long)tid * gridDim.x + blockIdx.x] = m;
-            a.pidx[(long)tid * gridDim.x + blockIdx.x] = mi;
         }
     }
 }
@@ -657,41 +502,6 @@ __global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __re
     *reinterpret_cast<u16x8*>(o + (long)b * K + e) = ob;
 }
 
-// q|k|v rows from KS fp32 partial slabs ws[ks][nb][rows] (fixed ks order), then RoPE on q and k
-// and the KV-cache append (the GV_QKV epilogue of gemv_body.h, modeling_gemma.py:197-198,259):
-// one thread per (b, rotary pair (d, d + 128) of a head)
-__global__ void k_mf_qkv_rope(const float* __restrict__ ws, int KS, GemvArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int rows = (a.I + 2 * a.nkv) * 256;
-    if (i >= a.nb * (rows / 2)) return;
-    const int b = i / (rows / 2), pu = i % (rows / 2);
-    const int hh = pu >> 7, d = pu & 127;
-    const long r0 = (long)hh * 256 + d;
-    float s0 = 0.f, s1 = 0.f;
-    for (int q = 0; q < KS; ++q) {
-        s0 += ws[((long)q * a.nb + b) * rows + r0];
-        s1 += ws[((long)q * a.nb + b) * rows + r0 + 128];
-    }
-    const float x0 = rbf(s0), x1 = rbf(s1);
-    const int kv_len = a.st->kv_len;
-    int pos = a.st->position;
-    if (pos < 0) pos = 0;
-    if (pos > a.max_pos - 1) pos = a.max_pos - 1;  // clamp (modeling_gemma.py:163-165)
-    const int nh = a.I;
-    if (hh < nh + a.nkv) {
-        const float c = bf2f(a.cosT[(long)pos * 128 + d]);
-        const float sn = bf2f(a.sinT[(long)pos * 128 + d]);
-        uint16_t* dst = hh < nh ? a.out + (long)b * nh * 256 + hh * 256
-                                : a.kc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh) * 256;
-        dst[d] = f2bf(rbf(x0 * c) + rbf(-x1 * sn));
-        dst[d + 128] = f2bf(rbf(x1 * c) + rbf(x0 * sn));
-    } else {
-        uint16_t* dst = a.vc + b * a.kv_b_stride + (long)kv_len * (a.nkv * 256) + (hh - nh - a.nkv) * 256;
-        dst[d] = f2bf(x0);
-        dst[d + 128] = f2bf(x1);
-    }
-}
-
 // h[b][n] = bf16(bf16(sum_ks ws[ks][b][n]) + h[b][n]), fixed ks order
 __global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N, uint16_t* __restrict__ h) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -701,14 +511,8 @@ __global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N
     h[i] = f2bf(rbf(s) + bf2f(h[i]));
 }
 
-// launch-shape override for measurement (tools/probes): PGMI_MF_MINB = smallest batch on MFMA
-int gemv_mf_min_batch() {
-    static const int v = [] {
-        const char* e = std::getenv("PGMI_MF_MINB");
-        return e ? std::atoi(e) : 3;
-    }();
-    return v;
-}
+// smallest lock-step batch whose decode projections run on MFMA (B <= 2: the v_dot2 GEMVs of gemv_body.h)
+int gemv_mf_min_batch() { return 3; }
 
 template <int MODE, int NR, int KW, int WK>
 static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
@@ -724,21 +528,7 @@ static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, floa
 
 static int groups_of(int units) { return (units + 15) / 16; }
 
-
-template <int MODE, int NR, int KSL, int D>
-static void launch_ms(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
-    const size_t lds = (size_t)a.nb * (KSL + 8) * sizeof(uint16_t);
-    static size_t attr = 0;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_ms<MODE, NR, KSL, D>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = lds;
-    }
-    hipLaunchKernelGGL((k_gemv_ms<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(256), lds, s, a, ws);
-}
-
-// waves: streaming waves per workgroup (4, or fewer to spread a short row count over more CUs;
-// GV_LOGITS keeps 4: its block reduction is laid out for 4 waves)
+// waves: streaming waves per workgroup (GV_LOGITS keeps 4: its block reduction is laid out for 4 waves)
 template <int MODE, int NR, int KSL, int D>
 static void launch_ml(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws, int waves = 4) {
     const size_t lds = (((size_t)a.nb * (KSL + 8) * 2 + 127) & ~(size_t)127) + (size_t)waves * D * NR * 16 * 256;
@@ -751,43 +541,25 @@ static void launch_ml(hipStream_t s, const GemvArgs& a, int blocks, int KS, floa
     hipLaunchKernelGGL((k_gemv_ml<MODE, NR, KSL, D>), dim3(blocks, KS), dim3(64 * waves), lds, s, a, ws);
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-
 // workgroups of 4 streaming waves: every group once, capped at `cap` workgroups (grid-stride)
 static int ms_blocks(int units, int cap) {
     const int wg = (groups_of(units) + 3) / 4;
     return wg < cap ? wg : cap;
 }
 
-// q|k|v: 2560 plain rows streamed over 4 K slices of 512 (320 waves where 80 row-pair groups
-// would leave most CUs idle), fp32 partials in ws, then RoPE + KV append in k_mf_qkv_rope
-void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* ws) {
-    if (!ws || env_int("PGMI_MF_QKV_SPLIT", 0) == 0) {  // default: the in-workgroup K split form (measured faster)
-        if (env_int("PGMI_MF_QKV_ROWS", 1)) {  // one row per lane, rotary pairs across lanes: 160 workgroups
-            GemvArgs r = a;
-            r.n_units = 2 * a.n_units;
-            launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
-        } else {
-            launch_mf<GV_QKV, 2, 256, 8>(s, a, groups_of(a.n_units), 1, nullptr);
-        }
-        return;
-    }
-    constexpr int KS = 4;
+// q|k|v: one weight row per lane, rotary pairs across lanes n / n + 8 (one shuffle in the
+// epilogue): 160 workgroups of 8 waves splitting K = 2048 (the pair-per-lane form made 80, and a
+// 4-way K split over workgroups with a separate RoPE kernel measured slower)
+void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
     GemvArgs r = a;
-    r.n_units = (a.I + 2 * a.nkv) * 256;  // weight rows
-    launch_ml<GV_RES, 1, 512, 6>(s, r, ms_blocks(r.n_units, 256), KS, ws);
-    const int n = a.nb * r.n_units / 2;
-    hipLaunchKernelGGL(k_mf_qkv_rope, dim3((n + 255) / 256), dim3(256), 0, s, ws, KS, a);
+    r.n_units = 2 * a.n_units;
+    launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
     // (4 streaming waves with a 3-deep ring measured fastest: 2 waves x 5 / 7 deep and 1 wave x 8 deep,
     // the same bytes in flight over fewer row streams, took the B = 8 step from 1.795 to 1.860-1.907 ms)
-    if (env_int("PGMI_MF_ML", 1)) launch_ml<GV_GEGLU, 2, 2048, 3>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
-    else launch_ms<GV_GEGLU, 2, 2048, 4>(s, a, ms_blocks(a.n_units, env_int("PGMI_MF_GU_CAP", 512)), 1, nullptr);
+    launch_ml<GV_GEGLU, 2, 2048, 3>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
 }
 
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
@@ -798,46 +570,26 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     r.x = o;
     r.norm_w = nullptr;
     // 128 workgroups of 8 waves splitting K (the q|k|v form) instead of 64 two-wave LDS-ring workgroups:
-    // B = 8 step 1.751-1.760 -> 1.718-1.721 ms (same-box A/B); PGMI_MF_O_MF=0 restores the ring form.
-    // (The same form for the K = 16384 down projection, 1,024 workgroups, measured slower: 1.79 ms.)
-    if (env_int("PGMI_MF_O_MF", 1)) {
-        launch_mf<GV_RES, 1, 256, 8>(s, r, groups_of(a.n_units), 1, nullptr);
-        return;
-    }
-    if (env_int("PGMI_MF_ML", 1)) {
-        // 2048 rows = 128 groups of 16: 4-wave workgroups would occupy only 32 CUs
-        static const int w = env_int("PGMI_MF_O_WAVES", 2);  // measured: 4 -> 1.828, 1 -> 1.812, 2 -> 1.807 ms per B = 8 step
-        const int waves = (w == 1 || w == 2) ? w : 4;
-        const int g = groups_of(a.n_units);
-        launch_ml<GV_RES, 1, 2048, 6>(s, r, (g + waves - 1) / waves, 1, nullptr, waves);
-    } else {
-        launch_ms<GV_RES, 1, 2048, 4>(s, r, ms_blocks(a.n_units, 1024), 1, nullptr);
-    }
+    // B = 8 step 1.751-1.760 -> 1.718-1.721 ms (same-box A/B).  (The same form for the K = 16384 down
+    // projection, 1,024 workgroups, measured slower: 1.79 ms.)
+    launch_mf<GV_RES, 1, 256, 8>(s, r, groups_of(a.n_units), 1, nullptr);
 }
 
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2048
-    if (env_int("PGMI_MF_ML", 1)) {
-        const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
-        launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
-        return blocks;
-    }
-    const int blocks = ms_blocks(a.n_units, max_blocks < 1024 ? max_blocks : 1024);
-    launch_ms<GV_LOGITS, 1, 2048, 4>(s, a, blocks, 1, nullptr);
+    const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
+    launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
     return blocks;
 }
 
 // residual projections; ws: fp32 scratch of KS x nb x N floats for the K split of K = 16384
 void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws) {
-    const bool ml = env_int("PGMI_MF_ML", 1) != 0;
     if (a.K == 2048) {
-        if (ml) launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
-        else launch_ms<GV_RES, 1, 2048, 4>(s, a, ms_blocks(a.n_units, 1024), 1, nullptr);
+        launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
         return;
     }
     if (a.K % 2048 == 0 && ws) {  // K slices of 2048 over grid.y, fp32 partials, fixed-order combine
         const int KS = a.K / 2048;
-        if (ml) launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), KS, ws);
-        else launch_ms<GV_RES, 1, 2048, 4>(s, a, ms_blocks(a.n_units, 1024), KS, ws);
+        launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), KS, ws);
         const int nn = a.nb * a.n_units;
         hipLaunchKernelGGL(k_mf_combine, dim3((nn + 255) / 256), dim3(256), 0, s, ws, KS, a.nb, a.n_units, a.out);
         return;

@@ -361,9 +361,14 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
             for (int j = 0; j < 4; ++j) { a[j] = p0[0][j]; a[4 + j] = p1[0][j]; }
 #pragma unroll
             for (int z = 1; z < kMaxSplit; ++z) {
-                const float m = z < split ? 1.f : 0.f;  // slabs in a fixed order; past `split`: + 0
+                // slabs in a fixed order; past `split` the sum is kept as is (a select after the
+                // loads, not a multiply by 0: Inf * 0 would turn the sum into NaN, -0 + 0 into +0)
+                const bool live = z < split;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) { a[j] += p0[z][j] * m; a[4 + j] += p1[z][j] * m; }
+                for (int j = 0; j < 4; ++j) {
+                    a[j] = live ? a[j] + p0[z][j] : a[j];
+                    a[4 + j] = live ? a[4 + j] + p1[z][j] : a[4 + j];
+                }
             }
             const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
             u16x8 o;

@@ -127,7 +127,6 @@ constexpr int kAttnPartStride = 16 * 256 + 32;  // floats per (b, kv head, chunk
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
 void attention_force_variant(int v);  // tuning hook (kernels_attn.hip); -1 = measured choice
-int attn_debug_stamps(long long* host, long n_words);  // stamps of the diagnostic attention variants
 
 // ---------------------------------------------------------------- misc
 // Fused consumer of a projection + residual: if split > 1, h = bf16(bf16(sum_z ws[z] (+bias)) + h)

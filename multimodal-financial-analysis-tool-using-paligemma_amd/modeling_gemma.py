@@ -286,6 +286,25 @@ def _positions_2d(position_ids, B, L) -> torch.Tensor:
     return pos.expand(B, L).contiguous()
 
 
+def _merged_positions(position_ids, mask, B, L) -> torch.Tensor:
+    """Host int64 (B, L) positions of a (patched) merge's output, read together with a check of
+    its attention mask in ONE device->host copy.  libpgmi attends every cached key with no
+    additive mask -- the reference's zero mask (modeling_gemma.py:506-511,
+    ablation_study_fixed.py:122-128) -- so a merge returning any non-zero mask entry is refused
+    rather than silently ignored."""
+    pid = torch.as_tensor(position_ids)
+    dev = pid.device if pid.device.type != "cpu" else (mask.device if torch.is_tensor(mask) else pid.device)
+    parts = [pid.detach().to(dev, torch.float64).reshape(-1)]
+    if torch.is_tensor(mask):
+        parts.append((mask != 0).any().to(dev, torch.float64).reshape(1))
+    host = torch.cat(parts).cpu()
+    if torch.is_tensor(mask) and host[-1].item() != 0:
+        raise NotImplementedError("libpgmi attends every cached key with no additive mask (the reference's zero "
+                                  "mask); the merge returned a non-zero attention mask")
+    n = parts[0].numel()
+    return _positions_2d(host[:n].reshape(pid.shape), B, L)
+
+
 class GemmaForCausalLM(nn.Module):
     """modeling_gemma.py:384-427."""
 
@@ -480,13 +499,21 @@ class PaliGemmaForConditionalGeneration(nn.Module):
                 img = eng.project(eng.vision(pixel_values))
             else:
                 img = torch.zeros(B, 0, inputs_embeds.shape[-1], dtype=inputs_embeds.dtype, device=dev)
-            merged, _mask, position_ids = self._merge_input_ids_with_image_features(
+            merged, mask, position_ids = self._merge_input_ids_with_image_features(
                 image_features=img, inputs_embeds=inputs_embeds.to(dev), input_ids=input_ids.to(dev),
                 attention_mask=attention_mask, kv_cache=kv_cache)
-            pos = _positions_2d(position_ids, B, L)
-            logits = _run_lm(eng, kv_cache, B, L, pos, embeds=merged, logits_rows=rows)
-            if mode == "lazy":
-                logits = LazyLogits(logits, eng.final_hidden(B * L), eng.lm_head, B, L)
+            pos = _merged_positions(position_ids, mask, B, L)
+            if kv_cache is not None and cache_len > 0 and L == 1 and bool((pos == pos[0, 0]).all()):
+                # a q_len == 1 step over a filled cache (the ablation harness's decode steps,
+                # ablation_study_fixed.py:215-221,239-243): the graphed decode step over the merged row
+                slab = kv_cache._ensure(eng, B, cache_len + 1)
+                logits = eng.decode_embeds(merged[:, 0], slab, cache_len, int(pos[0, 0]), logits=eng.logits_buffer(B),
+                                           graph=self.pgmi_use_graph).clone().unsqueeze(1)
+                kv_cache._len = cache_len + 1
+            else:
+                logits = _run_lm(eng, kv_cache, B, L, pos, embeds=merged, logits_rows=rows)
+                if mode == "lazy":
+                    logits = LazyLogits(logits, eng.final_hidden(B * L), eng.lm_head, B, L)
         elif cache_len == 0 or kv_cache is None:
             # prefill (modeling_gemma.py:532-535: positions 0..L-1), merge on the device
             img = eng.project(eng.vision(pixel_values)) if pixel_values is not None else None

@@ -65,6 +65,7 @@ SIGNATURES = {
     "pgmi_embed": (i32, [vp, vp, i32, vp, vp]),
     "pgmi_lm_forward": (i32, [vp, vp, vp, i32, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
     "pgmi_decode": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
+    "pgmi_decode_embeds": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
     "pgmi_set_prefill_graph": (i32, [vp, i32]),
     "pgmi_prefill_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_preprocess": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
@@ -79,7 +80,6 @@ SIGNATURES = {
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),
     "pgmi_tune_attention": (i32, [i32]),
-    "pgmi_debug_stamps": (i32, [i32, vp, ctypes.c_long]),
     "pgmi_sample_top_p": (i32, [vp, vp, i32, i32, f32, f32, vp, vp, vp, vp]),
     "pgmi_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]),
     "pgmi_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, f32, vp, vp]),

@@ -9,6 +9,7 @@ replacing Parameter objects needs an explicit unbind (pgmi_rebind on the top-lev
 """
 from __future__ import annotations
 
+import warnings
 import weakref
 
 import torch
@@ -46,9 +47,16 @@ def _fingerprint_of(sample):
     return tuple((p.data_ptr(), p._version, p.dtype) for p in sample)
 
 
+def _inv_fingerprint(inv_freq):
+    return None if inv_freq is None else (inv_freq.data_ptr(), inv_freq._version, inv_freq.dtype)
+
+
 class _Bound:
-    def __init__(self, engine, sample):
-        self.engine, self.sample, self.fp = engine, sample, _fingerprint_of(sample)
+    def __init__(self, engine, sample, inv_fp):
+        self.engine, self.sample, self.fp, self.inv_fp = engine, sample, _fingerprint_of(sample), inv_fp
+
+
+_warned_dtypes = set()
 
 
 def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
@@ -61,11 +69,22 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
     objects after the first forward needs unbind(module) (PaliGemmaForConditionalGeneration.pgmi_rebind)."""
     dev = _device_of(module)
     b = module.__dict__.get("_pgmi_bound")
+    inv_fp = _inv_fingerprint(inv_freq)
     if b is not None and b.fp == _fingerprint_of(b.sample) and b.engine.device == dev:
+        if b.inv_fp != inv_fp:
+            # the rotary inv_freq buffer changed (e.g. model.to(dtype) casts it, as the ablation's
+            # run_inference does, ablation_study_fixed.py:182): rebuild the RoPE table from its values
+            b.engine.prepare(inv_freq=inv_freq)
+            b.inv_fp = inv_fp
         return b.engine
     eng = Engine(cfg, device=dev, max_batch=DEFAULT_MAX_BATCH, max_seq=DEFAULT_MAX_SEQ)
     with torch.no_grad():
         for name, p in module.named_parameters():
+            if p.is_floating_point() and p.dtype != torch.bfloat16 and p.dtype not in _warned_dtypes:
+                _warned_dtypes.add(p.dtype)
+                warnings.warn(f"libpgmi computes in bf16: {p.dtype} parameters are rounded to bf16 "
+                              f"(the reference's fp16 default, utils.py / ablation_study_fixed.py:330, is not "
+                              f"reproduced)", stacklevel=3)
             full = prefix + name
             view = eng.views.get(full)
             if view is None:
@@ -76,7 +95,7 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
             if p.dtype == torch.bfloat16 and p.device == dev:
                 p.data = view
     eng.prepare(inv_freq=inv_freq)
-    module.__dict__["_pgmi_bound"] = _Bound(eng, _sample(module))
+    module.__dict__["_pgmi_bound"] = _Bound(eng, _sample(module), inv_fp)
     return eng
 
 

@@ -33,6 +33,22 @@ def broadcast_slab(slab: torch.Tensor, src: int = 0) -> None:
         dist.broadcast(slab, src=src)
 
 
+def exchange_comm_id(device: torch.device, src: int = 0) -> bytes:
+    """Rank `src` creates the RCCL unique id (pgmi_comm_unique_id, no GPU needed); the 128 bytes
+    travel to every rank over the torch.distributed group (on the device for nccl, on the host for
+    gloo).  Every rank returns the same bytes."""
+    from . import _native as N
+    lib = N.lib()
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if dist.get_rank() == src:
+        buf = (ctypes.c_uint8 * 128)()
+        N.check(lib.pgmi_comm_unique_id(buf), "pgmi_comm_unique_id")
+        uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+    t = uid.to(device) if dist.get_backend() == "nccl" else uid
+    dist.broadcast(t, src=src)
+    return bytes(t.cpu().tolist())
+
+
 class WeightComm:
     """An RCCL communicator owned by libpgmi (pgmi_comm_init), one per process / GPU."""
 
@@ -40,15 +56,8 @@ class WeightComm:
         from . import _native as N
         self.N, self.lib = N, N.lib()
         rank, world = dist.get_rank(), dist.get_world_size()
-        uid = torch.zeros(128, dtype=torch.uint8)
-        if rank == src:
-            buf = (ctypes.c_uint8 * 128)()
-            N.check(self.lib.pgmi_comm_unique_id(buf), "pgmi_comm_unique_id")
-            uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
         # only the 128-byte id travels over torch.distributed
-        t = uid.to(device) if dist.get_backend() == "nccl" else uid
-        dist.broadcast(t, src=src)
-        raw = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        raw = (ctypes.c_uint8 * 128)(*exchange_comm_id(device, src))
         h = ctypes.c_void_p()
         N.check(self.lib.pgmi_comm_init(device.index, world, rank, raw, ctypes.byref(h)), "pgmi_comm_init")
         self.comm = h

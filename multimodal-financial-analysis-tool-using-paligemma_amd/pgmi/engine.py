@@ -287,6 +287,20 @@ class Engine:
                 "pgmi_decode")
         return logits
 
+    def decode_embeds(self, embeds: torch.Tensor, kv: torch.Tensor, kv_len: int, position: int,
+                      logits: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
+        """The decode step over already-merged input rows (B, hidden) bf16 -- a caller's merge for
+        a q_len == 1 step (pgmi_decode_embeds); returns logits (B, V) fp32."""
+        self._ready()
+        e = embeds.to(self.device, torch.bfloat16).reshape(-1, self.cfgd["t_hidden"]).contiguous()
+        B = e.shape[0]
+        if logits is None:
+            logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        N.check(self.lib.pgmi_decode_embeds(self.ctx, e.data_ptr(), B, kv.data_ptr(), kv.shape[2], kv.shape[3], kv_len,
+                                            position, logits.data_ptr(), None, int(graph), self._s()),
+                "pgmi_decode_embeds")
+        return logits
+
     def set_prefill_graph(self, on: bool) -> None:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")

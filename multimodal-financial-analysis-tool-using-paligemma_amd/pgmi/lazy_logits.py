@@ -10,8 +10,13 @@ time anything other than the last row is read.  The last row of the materialised
 eager one, so every read sees one consistent tensor.
 
 Reads of the last position (`x[:, -1, :]`, `x[:, -1]`, `x[..., -1, :]`, `x[0, L-1]`) never
-materialise.  Everything else -- other indices, torch functions (`torch.argmax(x)`), tensor
-methods and operators -- materialises once and then acts on the real (B, L, V) tensor.
+materialise.  Everything else -- other indices, item assignment, torch functions
+(`torch.argmax(x)`), tensor methods and operators, in-place ones included -- materialises once and
+then acts on the real (B, L, V) tensor; every later read, last row included, indexes that tensor.
+LazyLogits is not a torch.Tensor subclass (`isinstance(x, torch.Tensor)` is False); the
+drop-in model's `pgmi_prefill_logits = "all"` returns a plain tensor.  One difference from a real
+tensor remains: a last-row view taken BEFORE materialisation is a view of the eager row, not of
+the later full tensor.
 """
 from __future__ import annotations
 
@@ -66,6 +71,9 @@ class LazyLogits:
             full = self._lm_head(self._hidden).view(self._B, self._L, self._V)
             full[:, -1:, :].copy_(self._last)  # one tensor: the eager last row wins
             self._full = full
+            # from here on the last row IS a view of the full tensor, so in-place ops on either
+            # (logits.div_(t), logits[:, -1, :] /= t) are seen by every later read
+            self._last = full[:, -1:, :]
             self._hidden = None
         return self._full
 
@@ -87,10 +95,19 @@ class LazyLogits:
         return (idx[0], 0) + tuple(idx[2:])
 
     def __getitem__(self, idx):
+        if self._full is not None:
+            return self._full[idx]
         li = self._last_row_index(idx)
         if li is not None:
             return self._last[li]
         return self.materialize()[idx]
+
+    def __setitem__(self, idx, value):
+        """Item assignment acts on the real tensor (materialises first, as a (B, L, V) tensor
+        would hold every row)."""
+        if isinstance(value, LazyLogits):
+            value = value.materialize()
+        self.materialize()[idx] = value
 
     # ---- everything else acts on the materialised tensor
     @classmethod

@@ -317,3 +317,53 @@ def greedy_generate(P, cfg, input_ids, pixel_values, n_tokens, eos=None):
         mask_len += 1
         logits = paligemma_decode(P, cfg, nxt, kv, mask_len)
     return np.stack(toks, axis=1), np.stack(step_logits, axis=1)
+
+
+def ablation_generate(P, cfg, input_ids, pixel_values, n_tokens, kv_mode):
+    """The ablation harness's greedy loop (ablation_study_fixed.py:168-251, run_inference with
+    temperature 0.0) under load_model_simple's two patches (:335-342):
+      * the patched merge (:99-142): with a filled cache EVERY query row sits at the single position
+        cumsum(mask)[:, -1:] (:130-133) and attends cached + q_len keys (:124-126); otherwise
+        positions 0..L-1 clamped to max_position_embeddings - 1 (:135-140);
+      * the patched rotary (:144-166): positions clamped, fp32 angles cast to bf16 (= rope_cos_sin).
+    KV mode: a discarded prefill (:194-199), then step 0 re-feeds prompt + pixels into the filled
+    cache, then one-token steps without pixels (:238-243).  no-KV mode: every step is a fresh
+    prefill over prompt + generated with the pixels (:244-251).
+    run_inference's `model = model.to(config["dtype"])` (:182) casts every floating buffer, the
+    rotary inv_freq included, so the angles come from bf16-rounded inverse frequencies.
+    Returns (tokens (n,), last-row logits (n, V))."""
+    ids0 = np.asarray(input_ids)
+    B, L = ids0.shape
+    t = cfg["text_config"]
+    max_pos = t.get("max_position_embeddings", 8192)
+    invf = bf16(inv_freq(t.get("head_dim", 256), t.get("rope_theta", 10000.0)))
+    feats = project(P, siglip_vision(P, cfg, pixel_values))
+    toks, steps = [], []
+    if kv_mode:
+        kv = KV()
+        emb = merge(P, cfg, feats, ids0)
+        gemma_forward(P, cfg, emb, np.broadcast_to(np.minimum(np.arange(L), max_pos - 1), (B, L)), kv, invf,
+                      all_logits=False)                                          # discarded prefill
+        cur, mask_len, with_px = ids0, L, True
+        for _ in range(n_tokens):
+            emb = merge(P, cfg, feats if with_px else None, cur)
+            q = cur.shape[1]
+            pos = np.full((B, q), mask_len, dtype=np.int64)                      # cumsum(mask)[:, -1:]
+            last = gemma_forward(P, cfg, emb, pos, kv, invf, all_logits=False)[:, -1, :]
+            nxt = np.argmax(last, axis=-1)
+            steps.append(last)
+            toks.append(nxt)
+            cur, mask_len, with_px = nxt.reshape(B, 1), mask_len + 1, False
+    else:
+        gen = []
+        for _ in range(n_tokens):
+            cur = np.concatenate([ids0, np.array(gen, dtype=np.int64).reshape(B, -1)], axis=1) if gen else ids0
+            n = cur.shape[1]
+            emb = merge(P, cfg, feats, cur)
+            last = gemma_forward(P, cfg, emb, np.broadcast_to(np.minimum(np.arange(n), max_pos - 1), (B, n)), KV(),
+                                 invf, all_logits=False)[:, -1, :]
+            nxt = np.argmax(last, axis=-1)
+            steps.append(last)
+            toks.append(nxt)
+            gen.append(int(nxt[0]))
+    return np.stack(toks, axis=1), np.stack(steps, axis=1)

@@ -17,6 +17,9 @@ What is captured:
   full_fp32.npz     the same token path teacher-forced in fp32 ("truth")
   full448_bf16.npz  PaliGemma-3B-448 shapes, bf16 prefill
   full_nokv_bf16.npz  KV cache disabled, ablation semantics (ablation_study_fixed.py:244-251)
+  small_ablation_bf16.npz  the same on the 2+2-layer model, every logit kept (the oracle's check)
+  full_ablation_bf16.npz  the ablation harness itself (run_inference with load_model_simple's two
+                    patches): KV mode 64 tokens incl. the step-0 prompt re-feed, no-KV mode 48 tokens
 """
 from __future__ import annotations
 
@@ -418,16 +421,81 @@ def make_long(pixels, n_tokens=256):
     print("full256_{bf16,fp32}.npz written")
 
 
+def make_ablation(n_kv=64, n_nokv=48, small=False):
+    """The paper's own harness (ablation_study_fixed.py:168-287 run_inference) on the reference model
+    with BOTH of load_model_simple's patches applied (:335-342: the merge and every layer's rotary
+    forward), bf16, greedy (temperature 0.0).
+
+    KV mode: the discarded prefill (:194-199), then step 0 re-feeds the whole prompt + pixels into the
+    filled cache -- every prompt row at the single position cumsum(mask)[:, -1:] = L (:130-133) and
+    attending 2L keys (:124-126) -- then q_len == 1 steps at positions L+t over 2L+t keys.
+    no-KV mode: every step re-runs vision + a bidirectional prefill over prompt + generated (:244-251).
+
+    torch.cuda.synchronize (:204,211,253) is stubbed: there is no GPU in this container."""
+    sys.path.insert(0, REF)
+    import ablation_study_fixed as AB
+    cfg = W.small_config() if small else W.full_config(224)
+    V = cfg["text_config"]["vocab_size"]
+    sidx = sample_idx(V)
+    ids = prompt_ids(cfg)
+    model, _ = build_model(cfg, torch.bfloat16)
+    model._merge_input_ids_with_image_features = types.MethodType(AB.patched_merge_input_ids_with_image_features, model)
+    for layer in model.language_model.model.layers:
+        layer.self_attn.rotary_emb.forward = types.MethodType(AB.patched_rotary_forward, layer.self_attn.rotary_emb)
+    tok = FakeTokenizer(ids, cfg["image_token_index"])
+    proc = RP.PaliGemmaProcessor(tok, W.num_image_tokens(cfg), cfg["vision_config"]["image_size"])
+    sync = torch.cuda.synchronize
+    torch.cuda.synchronize = lambda *a, **k: None
+    res = {"ids": ids, "sample_idx": sidx}
+    try:
+        for mode, n in (("kv", n_kv), ("nokv", n_nokv)):
+            calls = []
+            orig_forward = model.forward
+
+            def spy(*a, **k):
+                out = orig_forward(*a, **k)
+                calls.append(out["logits"][:, -1, :].detach().float().clone())
+                return out
+
+            model.forward = spy
+            t0 = time.time()
+            try:
+                with torch.no_grad():
+                    r = AB.run_inference(model, proc, COCO[0], "p",
+                                         {"dtype": torch.bfloat16, "kv_cache": mode == "kv", "max_tokens": n,
+                                          "temperature": 0.0}, return_tokens=True)
+            finally:
+                del model.forward
+            toks = np.array(r["token_ids"], dtype=np.int64).reshape(-1)
+            step_logits = torch.cat(calls[1:], 0).numpy()      # calls[0] is the discarded prefill
+            assert step_logits.shape[0] == n == toks.shape[0]
+            print(f"ablation {mode}: {n} tokens in {time.time() - t0:.1f}s: {toks.tolist()[:24]}...")
+            s = summarize_steps(step_logits, sidx)
+            res.update({f"{mode}_tokens": toks, **{f"{mode}_{k}": v for k, v in s.items()}})
+            if small:  # every logit of every step (small vocabulary): the oracle's CPU check
+                res[f"{mode}_logits"] = bits(torch.from_numpy(step_logits))
+            if mode == "kv":
+                res["kv_prefill_topk_idx"], res["kv_prefill_topk_val"] = topk(calls[0].numpy(), 8)
+    finally:
+        torch.cuda.synchronize = sync
+    name = "small_ablation_bf16.npz" if small else "full_ablation_bf16.npz"
+    np.savez_compressed(os.path.join(HERE, name), **res)
+    print(name, "written")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["batch8", "long"], default=None,
-                    help="generate only the round-2 fixtures (full_batch8 / full256)")
+    ap.add_argument("--only", choices=["batch8", "long", "ablation"], default=None,
+                    help="generate only one later round's fixtures (full_batch8 / full256 / full_ablation)")
     a = ap.parse_args()
     torch.set_num_threads(8)
-    px = make_pixels() if a.only != "batch8" else None
+    px = make_pixels() if a.only not in ("batch8", "ablation") else None
     if a.only == "batch8":
         make_batch_images()
+    elif a.only == "ablation":
+        make_ablation(16, 8, small=True)
+        make_ablation()
     elif a.only == "long":
         make_long(px)
     else:
@@ -436,3 +504,5 @@ if __name__ == "__main__":
             make_full(px)
             make_batch_images()
             make_long(px)
+            make_ablation(16, 8, small=True)
+            make_ablation()

@@ -162,3 +162,37 @@ def test_shard_range():
             assert got[0][0] == 0 and got[-1][1] == n
             assert all(got[i][1] == got[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in got) - min(h - l for l, h in got) <= 1
+
+
+def test_merged_positions_and_mask_check():
+    """The patched-merge path reads a merge's positions and checks its mask in one host copy; a
+    non-zero additive mask is refused (libpgmi attends every cached key, the reference's zero mask)."""
+    import modeling_gemma as MG
+    m = torch.zeros(1, 1, 1, 577, dtype=torch.bfloat16)
+    pos = MG._merged_positions(torch.tensor([[289.0]]), m, 1, 1)          # decode: float cumsum
+    assert pos.tolist() == [[289]] and pos.dtype == torch.int64
+    pos = MG._merged_positions(torch.tensor([[288]]), torch.zeros(1, 1, 288, 576), 1, 288)  # step-0 re-feed
+    assert pos.shape == (1, 288) and bool((pos == 288).all())
+    pos = MG._merged_positions(torch.arange(5).unsqueeze(0), torch.zeros(1, 1, 5, 5), 1, 5)
+    assert pos.tolist() == [[0, 1, 2, 3, 4]]
+    with pytest.raises(NotImplementedError):
+        MG._merged_positions(torch.arange(5).unsqueeze(0), torch.full((1, 1, 5, 5), -1e4), 1, 5)
+
+
+def test_ablation_patches_restated_match_reference_semantics():
+    """tests_helpers' restated ablation merge: a filled cache puts every query row at cumsum(mask)[-1]
+    and widens the mask to cached + q_len keys (ablation_study_fixed.py:121-133)."""
+    import types
+    from tests_helpers import ablation_merge
+    cfg = types.SimpleNamespace(image_token_index=9, hidden_size=4,
+                                text_config=types.SimpleNamespace(max_position_embeddings=8))
+    self = types.SimpleNamespace(config=cfg, pad_token_id=0)
+    ids = torch.tensor([[9, 9, 5, 0, 6]])
+    emb = torch.ones(1, 5, 4)
+    img = torch.full((1, 2, 4), 2.0)
+    kv = types.SimpleNamespace(num_items=lambda: 5)
+    out, mask, pos = ablation_merge(self, img, emb, ids, torch.ones(1, 5, dtype=torch.long), kv)
+    assert mask.shape == (1, 1, 5, 10) and pos.tolist() == [[5]]
+    assert torch.equal(out[0, :, 0], torch.tensor([1.0, 1.0, 1.0, 0.0, 1.0]))  # 2 / sqrt(4) = 1; pad row zero
+    out, mask, pos = ablation_merge(self, img, emb, ids, torch.ones(1, 12, dtype=torch.long)[:, :5], None)
+    assert mask.shape == (1, 1, 5, 5) and pos.tolist() == [[0, 1, 2, 3, 4]]

@@ -61,3 +61,27 @@ def test_inference_loop_pattern():
     nt = torch.argmax(x[:, -1, :], dim=-1, keepdim=True)
     assert torch.equal(nt, last[:, 0].argmax(-1, keepdim=True))
     assert calls == []
+
+
+def test_in_place_ops_after_materialization_reach_every_read():
+    """A real (B, L, V) tensor has one storage: in-place ops on it, or writes through a last-row
+    view, must be seen by later last-row reads."""
+    x, full, last, calls = _make()
+    x.materialize()
+    x.div_(2.0)                                   # tensor method through __getattr__, in place
+    assert torch.equal(x[:, -1, :], last[:, 0] / 2)
+    v = x[:, -1, :]
+    v.mul_(4.0)                                   # write through a last-row view
+    assert torch.equal(x.materialize()[:, -1], last[:, 0] * 2)
+    assert torch.equal(x[:, 0, :], full[:, 0] / 2)
+    assert calls == [B * L]
+
+
+def test_item_assignment_materializes():
+    x, full, last, calls = _make()
+    x[:, -1, :] = 0.0
+    assert x.is_materialized and calls == [B * L]
+    assert torch.equal(x[:, -1, :], torch.zeros(B, V))
+    assert torch.equal(x[:, 0, :], full[:, 0])
+    x[:, 1, 2] /= 4
+    assert torch.equal(x[:, 1, 2], full[:, 1, 2] / 4)

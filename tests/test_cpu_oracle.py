@@ -165,3 +165,28 @@ def test_resize_oracle_bit_exact_vs_pil(golden_dir):
     # the COCO fixture agrees with the pixels.npz one (the reference's process_images input)
     px = np.load(os.path.join(golden_dir, "pixels.npz"))
     assert np.array_equal(g["coco0_224"], px["u8_0_224"]) and np.array_equal(g["coco0_448"], px["u8_0_448"])
+
+
+@pytest.mark.parametrize("mode", ["kv", "nokv"])
+def test_ablation_harness(small, gold, golden_dir, mode):
+    """The ablation harness (ablation_study_fixed.py:168-251 with load_model_simple's two patches)
+    restated by O.ablation_generate vs the reference's own run of it (small_ablation_bf16.npz):
+    KV mode incl. the step-0 prompt re-feed at one position over 2L keys, and no-KV mode."""
+    cfg, P = small
+    g = np.load(os.path.join(golden_dir, "small_ablation_bf16.npz"))
+    ref = O.from_bits(g[f"{mode}_logits"])
+    n = ref.shape[0]
+    px = O.bf16(O.from_bits(gold["pixels_bits"]))
+    toks, steps = O.ablation_generate(P, cfg, g["ids"], px, n, kv_mode=(mode == "kv"))
+    per_step = [rel(steps[0, t], ref[t]) for t in range(n)]
+    assert max(per_step) < 2e-2, per_step
+    diff = np.nonzero(toks[0] != g[f"{mode}_tokens"])[0]
+    assert len(diff) == 0 or g[f"{mode}_margin"][diff[0]] < 0.25
+
+
+def test_ablation_fixture_consistency(golden_dir):
+    """The full-size ablation fixture: greedy tokens are the stored top-1 of every step."""
+    g = np.load(os.path.join(golden_dir, "full_ablation_bf16.npz"))
+    for mode, n in (("kv", 64), ("nokv", 48)):
+        assert g[f"{mode}_tokens"].shape == (n,)
+        assert np.array_equal(g[f"{mode}_topk_idx"][:, 0], g[f"{mode}_tokens"])

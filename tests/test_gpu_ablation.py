@@ -1,0 +1,168 @@
+"""The paper's own benchmark harness through the drop-in model, at the FULL PaliGemma-3B / 224 px
+shapes: ablation_study_fixed.py:168-287 (run_inference) with load_model_simple's two monkey-patches
+installed (:335-342: the merge and every layer's rotary forward; restated in tests_helpers), bf16,
+greedy, against the reference's own run of the same harness (tests/golden/full_ablation_bf16.npz,
+make_golden.py make_ablation):
+
+  * KV mode, 64 tokens: the discarded prefill, then step 0 re-feeds the whole prompt + pixels into
+    the filled cache -- every prompt row at the ONE position cumsum(mask)[:, -1:] = L, attending
+    2L keys -- then q_len == 1 steps at position L + t over 2L + t keys, which the drop-in routes
+    to the graph-replayed decode step over the merged row (pgmi_decode_embeds);
+  * no-KV mode, 48 tokens: every step re-runs the vision tower and a bidirectional prefill over
+    prompt + generated tokens.
+run_inference's `model.to(config["dtype"])` (:182) also casts the rotary inv_freq buffers to bf16;
+the drop-in rebuilds its RoPE table from the cast buffer, as the reference's rotary reads it.
+
+Parity rules as tests/test_gpu_full.py: teacher-forced on the reference's tokens, |delta| <= 0.25 at
+the reference's top-8 of every step and the argmax equal wherever the reference's top-2 margin
+exceeds 0.25; free-running tokens equal up to the first step where the reference is indecisive."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import weights as W
+from tests_helpers import install_ablation_patches, pixels_from_u8, remove_ablation_patches
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+SEED = 1234
+
+
+@pytest.fixture(scope="module")
+def G(golden_dir):
+    return {"ab": np.load(os.path.join(golden_dir, "full_ablation_bf16.npz")),
+            "px": np.load(os.path.join(golden_dir, "pixels.npz"))}
+
+
+@pytest.fixture(scope="module")
+def model():
+    import modeling_gemma as MG
+    import utils as U
+    cfg = W.full_config(224)
+    pcfg = MG.PaliGemmaConfig(**{k: v for k, v in cfg.items() if k not in ("bos_token_id", "eos_token_id")})
+    m = U.build_model(pcfg, device="cuda")
+    m.tie_weights()
+    eng = m._pgmi_engine()
+    eng.fill_synthetic(SEED, W.init_policy)
+    eng.prepare()
+    install_ablation_patches(m)
+    yield m.eval()
+    remove_ablation_patches(m)
+    del m
+    torch.cuda.empty_cache()
+
+
+def run_harness(model, ids, px, kv_mode, n, teacher=None):
+    """run_inference's loop (ablation_study_fixed.py:185-251) with temperature 0.0; teacher: feed
+    these tokens instead of the argmax.  Returns (last-row logits of every step (n, V), argmaxes,
+    the discarded prefill's last row)."""
+    import modeling_gemma as MG
+    model = model.to(torch.bfloat16)   # :182 -- casts the rotary inv_freq buffers to bf16 as well
+    ids0, mask0, px0 = ids, torch.ones_like(ids), px.to(torch.bfloat16)
+    input_ids, mask, pixel = ids0, mask0, px0
+    kv = MG.KVCache() if kv_mode else None
+    pre = model(input_ids=input_ids, pixel_values=pixel, attention_mask=mask, kv_cache=kv)["logits"][:, -1, :].clone()
+    gen, steps, picks = [], [], []
+    for step in range(n):
+        out = model(input_ids=input_ids, pixel_values=pixel, attention_mask=mask, kv_cache=kv)
+        if kv_mode:
+            kv = out["kv_cache"]
+        last = out["logits"][:, -1, :]
+        steps.append(last.clone())
+        nxt = torch.argmax(last, dim=-1, keepdim=True)
+        assert nxt.size() == (1, 1)
+        picks.append(nxt)
+        if teacher is not None:
+            nxt = torch.tensor([[int(teacher[step])]], device=ids.device)
+        gen.append(nxt.squeeze(0))
+        if kv_mode:
+            input_ids = gen[-1].unsqueeze(-1)
+            mask = torch.cat([mask, torch.ones((1, 1), device=input_ids.device)], dim=-1)
+            pixel = None
+        else:
+            input_ids = torch.cat([ids0, torch.cat(gen, dim=-1).unsqueeze(0)], dim=-1)
+            mask = torch.cat([mask0, torch.ones((1, len(gen)), device=input_ids.device)], dim=-1)
+            pixel = px0
+    if kv_mode:
+        assert kv.num_items() == 2 * ids0.shape[1] + n - 1
+    return torch.cat(steps, 0), torch.cat(picks, 0).reshape(-1).cpu().numpy(), pre
+
+
+def _check(logits, picks, g, mode):
+    top = torch.gather(logits, 1, torch.from_numpy(g[f"{mode}_topk_idx"]).cuda()).cpu().numpy()
+    err = np.abs(top - g[f"{mode}_topk_val"])
+    assert err.max() <= 0.25, (mode, err.max(), int(err.max(1).argmax()))
+    ref = g[f"{mode}_tokens"].reshape(-1)
+    decisive = g[f"{mode}_margin"] > 0.25
+    assert np.array_equal(picks[decisive], ref[decisive]), (mode, np.nonzero(picks != ref)[0][:8])
+
+
+@torch.no_grad()
+def test_ablation_kv_mode_teacher_forced(model, G):
+    g = G["ab"]
+    ids = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    eng = model._pgmi_engine()
+    calls = []
+    orig = eng.decode_embeds
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    eng.decode_embeds = counting
+    try:
+        n = len(g["kv_tokens"])
+        logits, picks, pre = run_harness(model, ids, px, True, n, teacher=g["kv_tokens"])
+    finally:
+        del eng.decode_embeds
+    # every q_len == 1 step took the graphed decode step over the merged row
+    assert len(calls) == n - 1
+    top = torch.gather(pre[0], 0, torch.from_numpy(g["kv_prefill_topk_idx"][0]).cuda()).cpu().numpy()
+    assert np.abs(top - g["kv_prefill_topk_val"][0]).max() <= 0.25
+    _check(logits, picks, g, "kv")
+
+
+@torch.no_grad()
+def test_ablation_kv_mode_free_running(model, G):
+    g = G["ab"]
+    ids = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    _, picks, _ = run_harness(model, ids, px, True, len(g["kv_tokens"]))
+    ref = g["kv_tokens"].reshape(-1)
+    diff = np.nonzero(picks != ref)[0]
+    if len(diff):
+        assert g["kv_margin"][diff[0]] < 0.25, (diff[0], picks[:diff[0] + 2], ref[:diff[0] + 2])
+
+
+@torch.no_grad()
+def test_ablation_no_kv_mode_teacher_forced(model, G):
+    g = G["ab"]
+    ids = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    logits, picks, _ = run_harness(model, ids, px, False, len(g["nokv_tokens"]), teacher=g["nokv_tokens"])
+    _check(logits, picks, g, "nokv")
+
+
+@torch.no_grad()
+def test_patched_merge_nonzero_mask_is_refused(model, G):
+    """libpgmi attends every cached key with no additive mask: a merge returning a non-zero mask
+    is refused, not ignored."""
+    import types
+    import modeling_gemma as MG
+    g = G["ab"]
+    ids = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    base = model._merge_input_ids_with_image_features
+
+    def masked(self, *a, **k):
+        e, m, p = base(*a, **k)
+        return e, m - 1e4, p
+
+    model._merge_input_ids_with_image_features = types.MethodType(masked, model)
+    try:
+        with pytest.raises(NotImplementedError):
+            model(input_ids=ids, pixel_values=px, attention_mask=torch.ones_like(ids), kv_cache=MG.KVCache())
+    finally:
+        model._merge_input_ids_with_image_features = base

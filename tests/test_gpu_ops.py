@@ -212,3 +212,29 @@ def test_argmax_rows(eng, rows, V):
         N.check(eng.lib.pgmi_argmax(eng.ctx, yd.data_ptr(), rows, V, got.data_ptr(), N.stream_handle()))
         torch.cuda.synchronize()
         assert torch.equal(got.cpu(), y[1:].view(rows, V).argmax(-1))
+
+
+@pytest.mark.parametrize("variant", [0, 8, 41, 42, 21, 22, 44, 24])
+@pytest.mark.parametrize("B,Lq,Lk,H,Hkv,d,scale", [
+    (1, 256, 256, 16, 16, 72, 72 ** -0.5),     # SigLIP 224
+    (3, 17, 5, 16, 16, 72, 72 ** -0.5),        # fewer keys than one tile
+    (1, 288, 288, 8, 1, 256, 1 / 16),          # Gemma prefill (MQA)
+    (2, 33, 70, 8, 1, 256, 1 / 16),            # ragged, keys beyond queries (cache)
+    (1, 288, 576, 8, 1, 256, 1 / 16),          # the ablation's step-0 re-feed: 2L keys
+])
+def test_attention_forced_variant(eng, variant, B, Lq, Lk, H, Hkv, d, scale):
+    """Every prefill attention kernel the tuning hook (pgmi_tune_attention) can force, against the
+    oracle restatement (variants a head dim does not have fall back to the default tiled kernel)."""
+    from pgmi import _native as NN
+    rng = np.random.default_rng(Lq * 3 + Lk + d + variant)
+    q, k, v = rand(rng, B, Lq, H, d, scale=2.0), rand(rng, B, Lk, Hkv, d, scale=2.0), rand(rng, B, Lk, Hkv, d)
+    o = torch.empty((B, Lq, H, d), dtype=torch.bfloat16, device="cuda")
+    qt, kt, vt = bf(q), bf(k), bf(v)
+    NN.check(eng.lib.pgmi_tune_attention(variant))
+    try:
+        NN.check(eng.lib.pgmi_op_attention(eng.ctx, qt.data_ptr(), kt.data_ptr(), vt.data_ptr(), o.data_ptr(),
+                                           B, Lq, Lk, H, Hkv, d, scale, NN.stream_handle()))
+        torch.cuda.synchronize()
+    finally:
+        NN.check(eng.lib.pgmi_tune_attention(-1))
+    assert rel_l2(np32(o), _attn_ref(q, k, v, scale)) < 1e-2

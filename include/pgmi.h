@@ -202,9 +202,22 @@ int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* str
  * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles, 30-35 warp-specialised panel tiles);
  * cfg < 0 restores the automatic (measured) plan. */
 int pgmi_tune_gemm(int cfg, int split);
+/* Tuning hook: the same for ONE GEMM shape (M x N x K, dual = the gate|up GeGLU form) while every
+ * other shape keeps its plan (in-situ sweeps of a whole forward); cfg < 0 removes the override.
+ * Split-K partials that a consumer reduces (out_proj, fc2, down: the residual + norm kernel) are
+ * limited to 16 slabs. */
+int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split);
+/* Reads `bytes` at device address p with `blocks` workgroups so they sit in the Infinity Cache
+ * (measurement of the decode-step prefetch; the step itself issues its own). */
+int pgmi_op_prefetch(pgmi_ctx* ctx, const void* p, long long bytes, int blocks, void* stream);
+/* Decode step: per layer, stream the first `bytes_per_layer` of its gate|up weights (half from the
+ * gate rows, half from the up rows) into the Infinity Cache on a side stream, beside the layer's
+ * q|k|v / attention / o_proj kernels (which leave HBM mostly idle); 0 = off. */
+int pgmi_set_decode_prefetch(pgmi_ctx* ctx, long long bytes_per_layer, int blocks);
 
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
- * LDS-resident scores, 8 = the same with every K/V load issued up front (head_dim 256, <= 320 keys), RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
+ * LDS-resident scores, 7 = one pass with K/V loaded once and scores in registers (head_dim 72, <= 256 keys),
+ * 8 = the same 16-row kernel with every K/V load issued up front (head_dim 256, <= 320 keys), RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
  * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); -1 restores the measured choice. */
 int pgmi_tune_attention(int variant);
 

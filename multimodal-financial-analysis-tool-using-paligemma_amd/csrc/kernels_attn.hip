@@ -641,6 +641,149 @@ __global__ void __launch_bounds__(64 * RG * KSPL) k_attn_fa(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- prefill, short key range, one pass
+// SigLIP at 224 px (256 keys, d 72): one 4-wave workgroup per 16 query rows of one head; wave w owns
+// keys [64 w, 64 w + 64).  Every load of the workgroup is issued before the first is consumed: Q and
+// the wave's K fragments straight into registers (MFMA layout, L2-served: each head's K/V is read by
+// its 16 workgroups), V by LDS-DMA into a dense [key][80] image (160-B rows: the transposed P.V reads
+// are bank-conflict free).  Scores stay in registers (no second pass over the keys); the exact
+// softmax's row max and sum meet across the 4 waves in LDS in a fixed order; each wave multiplies its
+// own keys' p = bf16(exp(s - M) / L) by V, and the 4 partial O tiles are summed in a fixed order and
+// rounded once -- the rounding points of k_attn_fa (s = bf16(bf16(k.q) * scale), p rounded after
+// normalisation, O rounded once), one global round trip instead of one per 32-key tile and pass.
+template <int HD, int MAXT>
+__global__ void __launch_bounds__(256) k_attn_short(AttnArgs a) {
+    using I = FAInfo<HD>;
+    constexpr int KS = I::KS, CT = I::CT, CH = I::CH;
+    constexpr int W = 4, KPW = 16 * MAXT, NK = W * KPW;
+    constexpr int VRS = CT * 16, VCH = VRS / 8;  // V image row: CT 16-column tiles, VCH 16-B chunks
+    static_assert(MAXT % 2 == 0, "whole 32-key P.V chunks per wave");
+    __shared__ __attribute__((aligned(16))) uint16_t Vl[NK * VRS];
+    __shared__ float red[2][W][16];
+    __shared__ __attribute__((aligned(16))) f32x4 ob[W - 1][CT][64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int b = blockIdx.z, kvh = blockIdx.y;
+    const int row0 = blockIdx.x * 16, nrows = a.Lq * a.G;
+    const int qi = row0 + li;
+    const bool qvalid = qi < nrows;
+    const int qpos = qvalid ? qi / a.G : 0, qhead = kvh * a.G + (qvalid ? qi % a.G : 0);
+    const uint16_t* qrow = a.q + b * a.q_b_stride + (long)qpos * a.q_row_stride + qhead * a.q_head_stride;
+    const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
+    const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
+    const int key0 = wave * KPW;
+
+    // ---- loads: Q and this wave's K fragments (registers), then the V image (LDS-DMA, all waves)
+    short8 qf[KS], kf[MAXT][KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) qf[kk] = load_frag<HD>(qrow, qvalid, kk, lane);
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+        int key = key0 + 16 * t + li;
+        key = key < a.Lk ? key : a.Lk - 1;  // rows past the keys: a valid row, score masked below
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) kf[t][kk] = load_frag<HD>(kbase + (long)key * a.k_row_stride, true, kk, lane);
+    }
+    const int vrows = (a.Lk + 31) & ~31;                  // whole 32-key chunks; rows * VCH is a multiple of 64
+    const int n_ins = vrows * VCH / 64;
+    for (int i = wave; i < n_ins; i += W) {
+        const int e = i * 64 + lane;
+        int key = e / VCH, ch = e % VCH;
+        key = key < a.Lk ? key : a.Lk - 1;               // p = 0 there
+        ch = ch < CH ? ch : CH - 1;                        // pad columns (never stored): a copy of the last chunk
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbase + (long)key * a.v_row_stride + ch * 8),
+                                         (__attribute__((address_space(3))) void*)(Vl + i * 64 * 8), 16, 0, 0);
+    }
+
+    // ---- S^T = K Q^T for the wave's keys: lane holds keys 16 t + 4 g + r of query li
+    float sc[MAXT][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            if (kk & 1) a1 = mfma16(kf[t][kk], qf[kk], a1);
+            else a0 = mfma16(kf[t][kk], qf[kk], a0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int key = key0 + 16 * t + 4 * g + r;
+            const float v = rbf(rbf(a0[r] + a1[r]) * a.scale);
+            sc[t][r] = key < a.Lk ? v : -INFINITY;
+            mx = fmaxf(mx, sc[t][r]);
+        }
+    }
+    // ---- exact softmax statistics: lane groups g, then the 4 waves in a fixed order
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (g == 0) red[0][wave][li] = mx;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V DMAs landed (visible after the barrier)
+    __syncthreads();
+    const float M = fmaxf(fmaxf(red[0][0][li], red[0][1][li]), fmaxf(red[0][2][li], red[0][3][li]));
+    float sm = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            sc[t][r] = sc[t][r] == -INFINITY ? 0.f : fa_exp(sc[t][r] - M);
+            sm += sc[t][r];
+        }
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    if (g == 0) red[1][wave][li] = sm;
+    __syncthreads();
+    const float invl = 1.0f / (((red[1][0][li] + red[1][1][li]) + red[1][2][li]) + red[1][3][li]);
+
+    // ---- O = sum over this wave's 32-key chunks of bf16(p) . V (k_attn_fa's key order in the fragment)
+    f32x4 oacc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) oacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < MAXT / 2; ++ch) {
+        // chunks past the staged rows (keys >= Lk rounded up to 32) hold no V: p is 0 there, but
+        // the unwritten LDS could hold non-finite bit patterns (0 * NaN), so they are skipped
+        // (wave-uniform: no lane diverges)
+        if (key0 + 32 * ch >= vrows) break;
+        short8 pa;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pa[kt * 4 + j] = (short)f2bf(sc[2 * ch + kt][j] * invl);
+        const uint16_t* vb0 = Vl + (key0 + 32 * ch + 4 * g + (li >> 2)) * VRS + 4 * (li & 3);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vb0 + c * 16));
+            const s4v hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(vb0 + 16 * VRS + c * 16));
+            const short8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            oacc[c] = mfma16(pa, vb, oacc[c]);
+        }
+    }
+    // ---- the 4 partial O tiles, summed in wave order, rounded once
+    if (wave > 0) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) ob[wave - 1][c][lane] = oacc[c];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int q = 0; q < W - 1; ++q)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) oacc[c] += ob[q][c][lane];
+    uint16_t* orow[4];
+    attn_out_rows(a, b, kvh, row0 + 4 * g, nrows, orow);
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int d = c * 16 + li;
+        if (d >= HD) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (orow[r]) orow[r][d] = f2bf(oacc[c][r]);
+    }
+}
+
 template <int HD, int RG, int KSPL>
 static void launch_fa(hipStream_t s, const AttnArgs& a) {
     using I = FAInfo<HD>;
@@ -656,7 +799,8 @@ static void launch_fa(hipStream_t s, const AttnArgs& a) {
     hipLaunchKernelGGL((k_attn_fa<HD, RG, KSPL, 1>), grid, dim3(64 * RG * KSPL), lds, s, a);
 }
 
-// attention variant override (tuning hook pgmi_tune_attention): 0 = the 16-row kernel, 8 = the
+// attention variant override (tuning hook pgmi_tune_attention): 0 = the 16-row kernel, 7 = the
+// one-pass short-range kernel (HD 72, <= 256 keys), 8 = the
 // 16-row kernel with every load up front (HD 256, <= 320 keys), RK = the tiled kernel with RG = R,
 // KSPL = K (41, 42, 21, 22; 44 and 24 for HD 72); -1 = the measured choice in attention_prefill.
 // Every variant is forced and checked against the oracle by tests/test_gpu_ops.py.
@@ -694,8 +838,14 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         // few rows -> the 16-row kernel (Gemma) or more, smaller workgroups (SigLIP)
         const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
         if (head_dim == 256) v = rows <= 4096 ? (a.Lk <= 320 ? 8 : 0) : 42;
-        else v = rows <= 8192 ? 24 : 44;
+        else v = a.Lk <= 256 ? 7 : rows <= 8192 ? 24 : 44;
     }
+    if (v == 7 && head_dim == 72 && a.Lk <= 256) {
+        dim3 grid((a.Lq * a.G + 15) / 16, a.n_kv, a.B);
+        hipLaunchKernelGGL((k_attn_short<72, 4>), grid, dim3(256), 0, s, a);
+        return;
+    }
+    if (v == 7) v = head_dim == 256 ? 42 : 24;  // forced on a shape it does not cover: the tiled kernel
     if (v == 8 && head_dim == 256 && a.Lk <= 320) {
         // 16 query rows per workgroup, every K/V load issued up front (Lk <= 320)
         const size_t lds = (size_t)16 * ((a.Lk + 31) & ~31) * 2 + (size_t)2 * 32 * (256 + 16) * 2 + 2 * 4 * 16 * 4;

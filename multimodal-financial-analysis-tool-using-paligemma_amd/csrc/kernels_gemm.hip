@@ -398,6 +398,24 @@ __device__ __forceinline__ void vm_wait_tiles(int n) {
     }
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (linear block id lin = x +
+// y * gridDim.x -> XCD lin % 8; observed placement, used for speed only), and each XCD has its own
+// L2.  The (column tile nt, K slice z, row tile mt) triples are listed column-tile-major -- the row
+// tiles of one (nt, z) weight panel adjacent -- and the list is cut into 8 contiguous runs, one per
+// XCD (run x = the blocks lin % 8 == x, in order).  So the n_mt workgroups that read one weight panel
+// sit on one XCD and its L2 serves the panel to all but the first; only panels at a run boundary
+// are fetched by two XCDs.
+__device__ __forceinline__ void xcd_tile(int n_mt, int& mt, int& nt, int& z) {
+    const int S = gridDim.y;
+    const int G = gridDim.x * S;
+    const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const int x = lin & 7, j = lin >> 3, q = G >> 3, r = G & 7;
+    const int idx = x * q + (x < r ? x : r) + j;
+    mt = idx % n_mt;
+    z = (idx / n_mt) % S;
+    nt = idx / (n_mt * S);
+}
+
 template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
@@ -418,21 +436,12 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     const int wm = wave / WN, wn = wave % WN;
-    // tile coordinates: the M tiles of one N tile share an XCD (blocks b, b+8, ... do), so a
-    // weight tile is fetched from HBM once per XCD rather than once per M tile
-    const int b = blockIdx.x;
-    int mt, nt;
-    if ((n_nt & 7) == 0) {
-        const int j = b >> 3;
-        mt = j % n_mt;
-        nt = (j / n_mt) * 8 + (b & 7);
-    } else {
-        mt = b % n_mt;
-        nt = b / n_mt;
-    }
+    // tile coordinates: the row tiles of one weight panel on one XCD (xcd_tile)
+    int mt, nt, z;
+    xcd_tile(n_mt, mt, nt, z);
     const int m0 = mt * BM, n0 = nt * BN;
     const int nkt_total = (K + 63) / 64;
-    const int kt0 = blockIdx.y * kt_per_split;
+    const int kt0 = z * kt_per_split;
     int kt1 = kt0 + kt_per_split;
     if (kt1 > nkt_total) kt1 = nkt_total;
     const int nkt = kt1 - kt0;
@@ -577,7 +586,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
+                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
     } else if constexpr (EPI == EPI_ROPE) {
@@ -612,19 +621,11 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int b = blockIdx.x;
-    int mt, nt;
-    if ((n_nt & 7) == 0) {
-        const int j = b >> 3;
-        mt = j % n_mt;
-        nt = (j / n_mt) * 8 + (b & 7);
-    } else {
-        mt = b % n_mt;
-        nt = b / n_mt;
-    }
+    int mt, nt, z;
+    xcd_tile(n_mt, mt, nt, z);
     const int m0 = mt * BM, n0 = nt * BN;
     const int nkt_total = (K + 63) / 64;
-    const int kt0 = blockIdx.y * kt_per_split;
+    const int kt0 = z * kt_per_split;
     int kt1 = kt0 + kt_per_split;
     if (kt1 > nkt_total) kt1 = nkt_total;
     const int nkt = kt1 > kt0 ? kt1 - kt0 : 0;
@@ -794,7 +795,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) ws[((long)blockIdx.y * M + m) * N + n] = acc[0][i][j][r];
+                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
     } else if constexpr (EPI == EPI_ROPE) {
@@ -862,6 +863,29 @@ void gemm_force_plan(int cfg, int split) {
     g_force_split = split;
 }
 
+// per-shape plan overrides (tuning hook pgmi_tune_gemm_shape): in-situ sweeps of one GEMM of a
+// forward while the others keep their measured plans
+struct ShapePlan {
+    int M, N, K;
+    bool dual;
+    int cfg, split;
+};
+static ShapePlan g_shape_plans[16];
+static int g_n_shape_plans = 0;
+
+int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split) {
+    for (int i = 0; i < g_n_shape_plans; ++i)
+        if (g_shape_plans[i].M == M && g_shape_plans[i].N == N && g_shape_plans[i].K == K &&
+            g_shape_plans[i].dual == (dual != 0)) {
+            g_shape_plans[i] = g_shape_plans[--g_n_shape_plans];
+            break;
+        }
+    if (cfg < 0) return 0;
+    if (g_n_shape_plans >= 16) return -1;
+    g_shape_plans[g_n_shape_plans++] = {M, N, K, dual != 0, cfg, split < 1 ? 1 : split};
+    return 0;
+}
+
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
         static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
@@ -911,6 +935,10 @@ static Plan choose(int M, int N, int K, bool dual) {
     static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
     static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
+    for (int i = 0; i < g_n_shape_plans; ++i) {
+        const ShapePlan& o = g_shape_plans[i];
+        if (o.M == M && o.N == N && o.K == K && o.dual == dual) return mk((Cfg)o.cfg, o.split);
+    }
     for (const Entry& e : table)
         if (e.M == M && e.N == N && e.K == K && e.dual == dual) return mk(e.cfg, e.split);
     // lock-step decode batches as GEMMs (M <= 16 rows; tools/gemm_sweep.py b8_*
@@ -1114,7 +1142,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
     if (p.split > 1 && (size_t)p.split * M * N * sizeof(float) > ws_bytes) p.split = 1;
     if (p.split > 1 && N % 4 != 0) p.split = 1;  // the split-K epilogue works on 4 outputs per thread
     const long up_off = (long)up_offset_rows * ldw;
-    if (defer && p.split > 8) p.split = 8;  // the consumers (splitk_res_norm, rope_kv) reduce at most 8 slabs
+    if (defer && p.split > 16) p.split = 16;  // the consumers (splitk_res_norm, rope_kv) reduce at most 16 slabs
     if (defer && p.split > 1) {
         // partial slabs only: the consumer kernel (splitk_res_norm / rope_kv_append) reduces them
         switch (p.cfg) {

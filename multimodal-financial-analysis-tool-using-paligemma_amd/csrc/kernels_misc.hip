@@ -325,8 +325,8 @@ void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int spl
 // row -- residual h, the split-K partial slabs (up to kMaxSplit, clamped to the live ones and
 // weighted 0 past `split`), bias, and the norm's weight / bias -- is issued before the first is
 // consumed: one memory round trip per row instead of one per slab plus one after the reductions.
-constexpr int kMaxSplit = 8;
-template <bool LN>
+constexpr int kMaxSplit = 16;
+template <bool LN, int MS>
 __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict__ ws, int split, long slab,
                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ h,
                                                          const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
@@ -349,9 +349,9 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
         const uint16_t* he = reinterpret_cast<const uint16_t*>(&hv);
         if (split > 1) {
             const uint4 bv = ldg16(bias ? bias + c : h + row * D + c);  // (h: any valid address, unused)
-            f32x4 p0[kMaxSplit], p1[kMaxSplit];
+            f32x4 p0[MS], p1[MS];
 #pragma unroll
-            for (int z = 0; z < kMaxSplit; ++z) {
+            for (int z = 0; z < MS; ++z) {
                 const long zo = (long)(z < split ? z : 0) * slab + row * D + c;
                 p0[z] = *reinterpret_cast<const f32x4*>(ws + zo);
                 p1[z] = *reinterpret_cast<const f32x4*>(ws + zo + 4);
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(256) k_splitk_res_norm(const float* __restrict
 #pragma unroll
             for (int j = 0; j < 4; ++j) { a[j] = p0[0][j]; a[4 + j] = p1[0][j]; }
 #pragma unroll
-            for (int z = 1; z < kMaxSplit; ++z) {
+            for (int z = 1; z < MS; ++z) {
                 // slabs in a fixed order; past `split` the sum is kept as is (a select after the
                 // loads, not a multiply by 0: Inf * 0 would turn the sum into NaN, -0 + 0 into +0)
                 const bool live = z < split;
@@ -428,12 +428,19 @@ void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* 
         fprintf(stderr, "pgmi: splitk_res_norm: split %d > %d\n", split, kMaxSplit);
         std::abort();
     }
-    if (b)
-        hipLaunchKernelGGL(k_splitk_res_norm<true>, dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, w, b, eps,
-                           out, D);
-    else
-        hipLaunchKernelGGL(k_splitk_res_norm<false>, dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, w, b, eps,
-                           out, D);
+    // slab loads issued up front: as many register slots as the split needs (4, 8 or 16)
+#define SRN_(ln, ms) hipLaunchKernelGGL((k_splitk_res_norm<ln, ms>), dim3(rows), dim3(256), 0, s, ws, split, slab, bias, h, \
+                                        w, b, eps, out, D)
+    if (b) {
+        if (split <= 4) SRN_(true, 4);
+        else if (split <= 8) SRN_(true, 8);
+        else SRN_(true, 16);
+    } else {
+        if (split <= 4) SRN_(false, 4);
+        else if (split <= 8) SRN_(false, 8);
+        else SRN_(false, 16);
+    }
+#undef SRN_
 }
 
 // ---------------------------------------------------------------- patch im2col
@@ -631,6 +638,33 @@ __global__ void k_set_step(StepState* st, int kv_len, int position) {
 
 void set_step(hipStream_t s, StepState* st, int kv_len, int position) {
     hipLaunchKernelGGL(k_set_step, dim3(1), dim3(1), 0, s, st, kv_len, position);
+}
+
+// ---------------------------------------------------------------- cache prefetch
+// Reads [p, p + bytes) with plain (allocating) 16-B loads so the bytes sit in the die-level
+// Infinity Cache (256 MiB) when their consumer streams them: issued beside latency-bound kernels
+// that leave HBM idle (decode: q|k|v, attention, o_proj), it moves part of the next weight stream's
+// HBM time into that idle window.  The loaded values feed nothing but an impossible-branch store.
+__global__ void __launch_bounds__(256) k_prefetch(const uint4* __restrict__ p, long n16, unsigned* __restrict__ sink) {
+    unsigned acc = 0;
+    const long stride = (long)gridDim.x * 256 * 8;
+    for (long i = (long)blockIdx.x * 256 * 8 + threadIdx.x; i < n16; i += stride) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const long k = i + j * 256;
+            v[j] = p[k < n16 ? k : n16 - 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc ^= v[j].x ^ v[j].w;
+    }
+    if (acc == 0x9e3779b9u && threadIdx.x == 1023) sink[0] = acc;  // never true for threadIdx < 256
+}
+
+void prefetch(hipStream_t s, const void* p, long bytes, int blocks, unsigned* sink) {
+    const long n16 = bytes / 16;
+    if (n16 <= 0) return;
+    hipLaunchKernelGGL(k_prefetch, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint4*>(p), n16, sink);
 }
 
 }  // namespace pgmi

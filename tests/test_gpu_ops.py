@@ -214,10 +214,12 @@ def test_argmax_rows(eng, rows, V):
         assert torch.equal(got.cpu(), y[1:].view(rows, V).argmax(-1))
 
 
-@pytest.mark.parametrize("variant", [0, 8, 41, 42, 21, 22, 44, 24])
+@pytest.mark.parametrize("variant", [0, 7, 8, 41, 42, 21, 22, 44, 24])
 @pytest.mark.parametrize("B,Lq,Lk,H,Hkv,d,scale", [
     (1, 256, 256, 16, 16, 72, 72 ** -0.5),     # SigLIP 224
     (3, 17, 5, 16, 16, 72, 72 ** -0.5),        # fewer keys than one tile
+    (2, 100, 200, 16, 16, 72, 72 ** -0.5),     # ragged key count inside a wave's range
+    (8, 256, 256, 16, 16, 72, 72 ** -0.5),     # 8 images (configs[3] per GPU)
     (1, 288, 288, 8, 1, 256, 1 / 16),          # Gemma prefill (MQA)
     (2, 33, 70, 8, 1, 256, 1 / 16),            # ragged, keys beyond queries (cache)
     (1, 288, 576, 8, 1, 256, 1 / 16),          # the ablation's step-0 re-feed: 2L keys

@@ -207,13 +207,6 @@ int pgmi_tune_gemm(int cfg, int split);
  * Split-K partials that a consumer reduces (out_proj, fc2, down: the residual + norm kernel) are
  * limited to 16 slabs. */
 int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split);
-/* Reads `bytes` at device address p with `blocks` workgroups so they sit in the Infinity Cache
- * (measurement of the decode-step prefetch; the step itself issues its own). */
-int pgmi_op_prefetch(pgmi_ctx* ctx, const void* p, long long bytes, int blocks, void* stream);
-/* Decode step: per layer, stream the first `bytes_per_layer` of its gate|up weights (half from the
- * gate rows, half from the up rows) into the Infinity Cache on a side stream, beside the layer's
- * q|k|v / attention / o_proj kernels (which leave HBM mostly idle); 0 = off. */
-int pgmi_set_decode_prefetch(pgmi_ctx* ctx, long long bytes_per_layer, int blocks);
 
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
  * LDS-resident scores, 7 = one pass with K/V loaded once and scores in registers (head_dim 72, <= 256 keys),

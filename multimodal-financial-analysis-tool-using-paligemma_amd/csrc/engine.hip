@@ -110,11 +110,6 @@ struct pgmi_ctx {
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
     hipStream_t cap_stream = nullptr;
-    // decode-step weight prefetch into the Infinity Cache on a side stream (pgmi_set_decode_prefetch)
-    hipStream_t side = nullptr;
-    std::vector<hipEvent_t> pf_events;  // one fork per layer + the join
-    long pf_bytes = 0;
-    int pf_blocks = 64;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
     // identical pointer/shape arguments (a replay is the eager call: kernels read the same
@@ -348,8 +343,6 @@ int pgmi_destroy(pgmi_ctx* x) {
     clear_pgraphs(x);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->cap_stream) (void)hipStreamDestroy(x->cap_stream);
-    for (hipEvent_t e : x->pf_events) (void)hipEventDestroy(e);
-    if (x->side) (void)hipStreamDestroy(x->side);
     delete x;
     return 0;
 }
@@ -918,21 +911,9 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
     if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
     else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
-    const bool pf = x->pf_bytes > 0 && x->side && (int)x->pf_events.size() >= c.t_layers + 1;
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-        if (pf) {
-            // the layer's q|k|v, attention and o_proj leave HBM mostly idle: stream the first part of
-            // its gate|up weights into the Infinity Cache beside them (side stream, after the previous
-            // layer's down projection), so the GeGLU GEMV reads that part on-die
-            HIPCHK(hipEventRecord(x->pf_events[i], s));
-            HIPCHK(hipStreamWaitEvent(x->side, x->pf_events[i], 0));
-            const long half = std::min<long>(x->pf_bytes / 2, (long)c.t_intermediate * H * 2);
-            const uint16_t* gu = TL(x, i, "mlp.gate_proj.weight");
-            prefetch(x->side, gu, half, x->pf_blocks, x->lm_done);
-            prefetch(x->side, gu + (long)c.t_intermediate * H, half, x->pf_blocks, x->lm_done);
-        }
         gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
                  x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws, (fold && i == 0) ? &emb : nullptr);
         AttnArgs a{};
@@ -955,10 +936,6 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
                      x->pidx, &nparts, x->lm_done, nx, x->step))
         argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
-    if (pf) {  // join the side stream (a captured fork must rejoin its origin)
-        HIPCHK(hipEventRecord(x->pf_events[c.t_layers], x->side));
-        HIPCHK(hipStreamWaitEvent(s, x->pf_events[c.t_layers], 0));
-    }
     return 0;
 }
 
@@ -1228,36 +1205,6 @@ int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* strea
 int pgmi_tune_gemm(int cfg, int split) {
     if (cfg >= kGemmCfgs || split < 0 || split > 32) return fail(PGMI_E_ARG, "bad GEMM plan");
     gemm_force_plan(cfg, split);
-    return 0;
-}
-
-int pgmi_set_decode_prefetch(pgmi_ctx* x, long long bytes_per_layer, int blocks) {
-    if (!x || bytes_per_layer < 0 || blocks < 1) return fail(PGMI_E_ARG, "bad argument");
-    if (bytes_per_layer > 0 && !x->side) {
-        int prev = 0;
-        HIPCHK(hipGetDevice(&prev));
-        HIPCHK(hipSetDevice(x->device));
-        hipError_t e = hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking);
-        for (int i = 0; e == hipSuccess && i <= x->c.t_layers; ++i) {
-            hipEvent_t ev;
-            e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-            if (e == hipSuccess) x->pf_events.push_back(ev);
-        }
-        HIPCHK(hipSetDevice(prev));
-        HIPCHK(e);
-    }
-    x->pf_bytes = (long)bytes_per_layer;
-    x->pf_blocks = blocks;
-    for (auto& kv : x->graphs)  // captured steps hold the old setting
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-    x->graphs.clear();
-    return 0;
-}
-
-int pgmi_op_prefetch(pgmi_ctx* x, const void* p, long long bytes, int blocks, void* stream) {
-    if (!x || !p || bytes < 0 || blocks < 1) return fail(PGMI_E_ARG, "bad argument");
-    prefetch((hipStream_t)stream, p, (long)bytes, blocks, reinterpret_cast<unsigned*>(x->lm_done));
-    LAUNCHCHK();
     return 0;
 }
 

@@ -904,13 +904,17 @@ static Plan choose(int M, int N, int K, bool dual) {
         // round 2: tools/gemm_sweep.py --cold (every call reads its weights from HBM, as the layer
         // loop does); W* = warp-specialised (k_gemm_w), P*s* = shallow rings
         {288, 2560, 2048, false, W64x64, 1},    // text q|k|v            10.8 us
-        {288, 2048, 2048, false, W64x64, 1},    // text o_proj           12.4 us
-        {288, 16384, 2048, true, W288w, 1},     // text gate|up (GeGLU)  44.6 us (was 55.8 cold)
-        {288, 2048, 16384, false, W288n, 8},    // text down             37.7 us
-        {256, 3456, 1152, false, W64x64, 1},    // vision q|k|v          10.7 us
-        {256, 1152, 1152, false, P32x64s4, 1},  // vision out_proj        8.9 us
+        // text rows, round 3 in situ (tools/probes/plan_sweep.py --target lm: the generate loop's whole
+        // language-model prefill timed per candidate, split partials reduced by the residual + RMSNorm)
+        {288, 2048, 2048, false, W128x128, 4},  // text o_proj           LM -45 us vs W64x64 unsplit
+        {288, 16384, 2048, true, W288n, 1},     // text gate|up (GeGLU)  LM -27 us vs W288w
+        {288, 2048, 16384, false, W128x128, 4}, // text down             LM -33 us vs W288n split 8
+        // vision rows: round 3, in situ (tools/probes/plan_sweep.py: the whole tower timed per
+        // candidate; split-K partials of out_proj / fc2 are reduced by the residual + LayerNorm kernel)
+        {256, 3456, 1152, false, P64x64s4, 1},  // vision q|k|v          tower -17 us vs W64x64
+        {256, 1152, 1152, false, P64x64s4, 3},  // vision out_proj       tower -38 us vs P32x64s4 unsplit
         {256, 4304, 1152, false, P96x64s4, 1},  // vision fc1 (+GELU)    11.0 us (exp/rcp GELU; was 16.4)
-        {256, 1152, 4304, false, P64x64s4, 3},  // vision fc2            18.4 us
+        {256, 1152, 4304, false, P96x64s4, 4},  // vision fc2            tower -19 us vs P64x64s4 split 3
         {256, 1152, 640, false, P64x32s4, 1},   // patch embedding        5.3 us (was 6.6 on P64x64)
         {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
         {1056, 2560, 2048, false, W128x128, 1}, // 448 px text q|k|v     21.3 us (P96x64s3 24.0 in the same sweep)

@@ -640,31 +640,4 @@ void set_step(hipStream_t s, StepState* st, int kv_len, int position) {
     hipLaunchKernelGGL(k_set_step, dim3(1), dim3(1), 0, s, st, kv_len, position);
 }
 
-// ---------------------------------------------------------------- cache prefetch
-// Reads [p, p + bytes) with plain (allocating) 16-B loads so the bytes sit in the die-level
-// Infinity Cache (256 MiB) when their consumer streams them: issued beside latency-bound kernels
-// that leave HBM idle (decode: q|k|v, attention, o_proj), it moves part of the next weight stream's
-// HBM time into that idle window.  The loaded values feed nothing but an impossible-branch store.
-__global__ void __launch_bounds__(256) k_prefetch(const uint4* __restrict__ p, long n16, unsigned* __restrict__ sink) {
-    unsigned acc = 0;
-    const long stride = (long)gridDim.x * 256 * 8;
-    for (long i = (long)blockIdx.x * 256 * 8 + threadIdx.x; i < n16; i += stride) {
-        uint4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const long k = i + j * 256;
-            v[j] = p[k < n16 ? k : n16 - 1];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc ^= v[j].x ^ v[j].w;
-    }
-    if (acc == 0x9e3779b9u && threadIdx.x == 1023) sink[0] = acc;  // never true for threadIdx < 256
-}
-
-void prefetch(hipStream_t s, const void* p, long bytes, int blocks, unsigned* sink) {
-    const long n16 = bytes / 16;
-    if (n16 <= 0) return;
-    hipLaunchKernelGGL(k_prefetch, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint4*>(p), n16, sink);
-}
-
 }  // namespace pgmi

@@ -80,8 +80,6 @@ SIGNATURES = {
     "pgmi_decode_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_tune_gemm": (i32, [i32, i32]),
     "pgmi_tune_gemm_shape": (i32, [i32, i32, i32, i32, i32, i32]),
-    "pgmi_op_prefetch": (i32, [vp, vp, ctypes.c_longlong, i32, vp]),
-    "pgmi_set_decode_prefetch": (i32, [vp, ctypes.c_longlong, i32]),
     "pgmi_tune_attention": (i32, [i32]),
     "pgmi_sample_top_p": (i32, [vp, vp, i32, i32, f32, f32, vp, vp, vp, vp]),
     "pgmi_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]),

@@ -1,0 +1,126 @@
+"""Probe: in-situ plan sweep of the prefill GEMMs and attention.  For each GEMM shape of the SigLIP
+tower (--target vision) or of the Gemma prefill (--target lm: the generate loop's prefill,
+pgmi_lm_forward with logits_rows 2) every candidate (tile config, split-K) is forced for that shape
+alone (pgmi_tune_gemm_shape) and the WHOLE tower / language model (graph-replayed) is timed, so
+split-K plans are charged with what their consumer (the residual + norm kernel) pays and every GEMM
+runs with the caches the layer loop leaves it.  Then the attention variants (pgmi_tune_attention).
+
+    python tools/probes/plan_sweep.py [--target vision|lm] [--batch 1] [--shapes ...] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "multimodal-financial-analysis-tool-using-paligemma_amd"))
+from pgmi import Engine, _native as N  # noqa: E402
+from pgmi.synthetic import init_policy, paligemma_3b_config  # noqa: E402
+
+CFGS = [14, 15, 17, 24, 25, 26, 27, 28, 29, 32, 34, 35]
+CFGS_LM = [6, 7, 9, 11, 17, 20, 22, 30, 31, 33, 34, 35]
+
+
+def time_tower(eng, px, iters):
+    eng.set_prefill_graph(True)  # drops captured graphs: the next calls re-plan
+    for _ in range(3):
+        eng.vision(px)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        eng.vision(px)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def time_lm(eng, args, iters):
+    eng.set_prefill_graph(True)
+    for _ in range(3):
+        out = eng.lm_forward(*args[0], **args[1])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        out = eng.lm_forward(*args[0], **args[1])
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--target", default="vision", choices=["vision", "lm"])
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--shapes", default=None)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    cfg = paligemma_3b_config(224)
+    eng = Engine(cfg, max_batch=a.batch, max_seq=320, max_kv=512)
+    eng.fill_synthetic(1234, init_policy)
+    eng.prepare()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    px = (torch.rand((a.batch, 3, 224, 224), generator=g, device="cuda") * 2 - 1).contiguous()
+    if a.target == "lm":
+        from pgmi.synthetic import prompt_ids
+        L, M = 288, 288 * a.batch
+        ids = torch.from_numpy(prompt_ids(cfg["image_token_index"], 256, cfg["text_config"]["vocab_size"])).cuda()
+        ids = ids.expand(a.batch, -1).contiguous()
+        feats = eng.project(eng.vision(px))
+        kv = eng.new_kv(a.batch, 512)
+        args = ((kv, 0, torch.arange(L).expand(a.batch, L)), dict(ids=ids, image_feats=feats, logits_rows=2))
+        shapes = {"qkv": (M, 2560, 2048, 0, [1, 2, 4]), "o": (M, 2048, 2048, 0, [1, 2, 4, 8]),
+                  "gateup": (M, 16384, 2048, 1, [1]), "down": (M, 2048, 16384, 0, [4, 8, 12, 16])}
+        base, ref = time_lm(eng, args, a.iters)
+        ref = ref.clone()
+        print(f"lm forward (current plans): {base:.1f} us", flush=True)
+        for name in (a.shapes or "qkv,o,gateup,down").split(","):
+            Mm, Nn, K, dual, splits = shapes[name]
+            rows = []
+            for c in CFGS_LM:
+                for sp in splits:
+                    N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, dual, c, sp))
+                    t, out = time_lm(eng, args, a.iters)
+                    err = float((out - ref).abs().max())
+                    rows.append((t, c, sp, err))
+            N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, dual, -1, 0))
+            rows.sort()
+            print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (d {e:.2g})" for t, c, sp, e in rows[:8]),
+                  flush=True)
+        return
+    M = 256 * a.batch
+    shapes = {"qkv": (M, 3456, 1152, [1, 2]), "out": (M, 1152, 1152, [1, 2, 3, 4, 6]),
+              "fc1": (M, 4304, 1152, [1, 2]), "fc2": (M, 1152, 4304, [1, 2, 3, 4, 6, 8, 12, 16])}
+    ref = eng.vision(px).clone()
+    base = time_tower(eng, px, a.iters)
+    print(f"tower (current plans): {base:.1f} us", flush=True)
+    for name in (a.shapes or "qkv,out,fc1,fc2,attn").split(","):
+        if name == "attn":
+            rows = []
+            for v in [41, 42, 21, 22, 44, 24]:
+                N.check(eng.lib.pgmi_tune_attention(v))
+                rows.append((time_tower(eng, px, a.iters), v))
+            N.check(eng.lib.pgmi_tune_attention(-1))
+            rows.sort()
+            print("attn: " + ", ".join(f"v{v}: {t:.1f}" for t, v in rows), flush=True)
+            continue
+        Mm, Nn, K, splits = shapes[name]
+        rows = []
+        for c in CFGS:
+            for sp in splits:
+                N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, 0, c, sp))
+                t = time_tower(eng, px, a.iters)
+                out = eng.vision(px)
+                torch.cuda.synchronize()
+                err = float((out.float() - ref.float()).abs().max())
+                rows.append((t, c, sp, err))
+        N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, 0, -1, 0))
+        rows.sort()
+        print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (d {e:.2g})" for t, c, sp, e in rows[:8]),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -557,9 +557,12 @@ void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
-    // (4 streaming waves with a 3-deep ring measured fastest: 2 waves x 5 / 7 deep and 1 wave x 8 deep,
-    // the same bytes in flight over fewer row streams, took the B = 8 step from 1.795 to 1.860-1.907 ms)
-    launch_ml<GV_GEGLU, 2, 2048, 3>(s, a, ms_blocks(a.n_units, 256), 1, nullptr);
+    // register-streamed MFMA form: 4 waves split K (512 each), 512 workgroups (2 per CU) dealing the
+    // 1,024 row groups grid-stride, so each stages its 8 normalised rows for two groups; same-box A/B
+    // (tools/b8_ab.sh) B = 8 step 1.737 -> 1.681 ms against the one-workgroup-per-CU LDS-DMA ring
+    // (k_gemv_ml, 4 waves x 3-deep rings); 256 / 384 / 1,024 workgroups and 2 or 8 K-split waves
+    // measured slower (1.746-2.051 ms)
+    launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
 }
 
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
@@ -576,6 +579,7 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
 }
 
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2048
+    // (the register-streamed form at 512 / 1,024 / 2,048 workgroups measured no faster: 1.741-1.768 ms)
     const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
     launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
     return blocks;
@@ -589,7 +593,10 @@ void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws) {
     }
     if (a.K % 2048 == 0 && ws) {  // K slices of 2048 over grid.y, fp32 partials, fixed-order combine
         const int KS = a.K / 2048;
-        launch_ml<GV_RES, 1, 2048, 6>(s, a, ms_blocks(a.n_units, 256), KS, ws);
+        // register-streamed MFMA form, 4 waves x 512 of each 2,048-wide K slice, 32 x 8 workgroups
+        // (every row group of a slice once): B = 8 step 1.737 -> 1.704 ms against the LDS-DMA ring
+        // (64 / 128 x 8 workgroups: 1.710 / 1.744)
+        launch_mf<GV_RES, 1, 512, 4>(s, a, 32, KS, ws);
         const int nn = a.nb * a.n_units;
         hipLaunchKernelGGL(k_mf_combine, dim3((nn + 255) / 256), dim3(256), 0, s, ws, KS, a.nb, a.n_units, a.out);
         return;

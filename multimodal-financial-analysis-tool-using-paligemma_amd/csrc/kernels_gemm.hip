@@ -15,6 +15,7 @@
 #include "launch.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace pgmi {
 
@@ -805,6 +806,229 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
     }
 }
 
+// ---------------------------------------------------------------- 8-phase GEMM (large M)
+// BM x 256 x 64 tiles (BM = 32 TM: 256 at TM 8), one 512-thread workgroup per CU, 8 waves in a
+// 2 (M) x 4 (N) grid, each wave TM x 4 MFMA tiles (TM x 2 gate + TM x 2 up for the dual GeGLU GEMM).
+// A wave's output splits into 4 quadrants (row half qa x column half qb); the LDS image of a K-tile
+// is cut the same way into 4 half-tiles -- A_qa = the qa-th row half of BOTH wave rows, B_qb = the
+// qb-th column half of all 4 wave columns -- so each phase reads exactly one A half and / or one B
+// half.  Two K-tiles per iteration, 8 phases (quadrant order (0,0) (0,1) (1,1) (1,0): every phase
+// but the first reuses the other operand's fragments from registers), each phase
+//   ds_read its fragments | LDS-DMA one half-tile of a later K-tile | [vmcnt] | s_barrier |
+//   lgkmcnt(0) | 16 MFMAs (setprio 1) | s_barrier
+// with the two wave rows staggered by one barrier (ping-pong: one wave of each SIMD in its MFMA
+// cluster while the other reads and stages) and four half-tiles in flight across every barrier:
+// cdna_hip_programming.md's 256^2 8-phase template, restated for this LDS image, with B0's
+// fragments kept in registers across the tile (one fewer fragment read per K-tile).
+// LDS rows are 128 B with the 16-B chunk XOR-swizzled by (row & 7) on the DMA's source address.
+template <int TM, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__ A, int lda,
+                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                    int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
+                                                    int n_mt) {
+    static_assert(TM % 2 == 0, "row halves of whole 16-row tiles");
+    constexpr bool DUAL = (EPI == EPI_GEGLU);
+    constexpr int H = TM / 2;                 // row tiles per quadrant
+    constexpr int BM = 32 * TM;
+    constexpr int HAR = 16 * TM;              // rows of an A half image (H tiles of each wave row)
+    constexpr int HAB = HAR * 128, HBB = 128 * 128;
+    constexpr int PA = HAR / 8, PB = 16;      // 1-KiB pieces per half
+    constexpr int GA = (PA + 7) / 8, GB = PB / 8;
+    constexpr int TB = 2 * HAB + 2 * HBB;     // one K-tile buffer: A0 A1 B0 B1
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm8[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int mt, nt, z;
+    xcd_tile(n_mt, mt, nt, z);
+    const int m0 = mt * BM, n0 = nt * (DUAL ? 128 : 256);
+    const int nkt_total = K / 64;
+    const int kt0 = z * kt_per_split;
+    const int kt1 = kt0 + kt_per_split < nkt_total ? kt0 + kt_per_split : nkt_total;
+    const int nkt = kt1 - kt0;
+    if (nkt <= 0) return;
+
+    // per-lane DMA sources (k = 0 of the tile's columns); piece p = wave + 8 i, pieces past the half
+    // repeat an earlier one (same bytes to the same LDS address)
+    const uint16_t* sa[2][GA];
+    int la[GA];
+    const uint16_t* sb[2][GB];
+    int lb[GB];
+    const int prow = lane >> 3, pch = lane & 7;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        int pc = wave + 8 * i;
+        if (pc >= PA) pc -= PA;
+        la[i] = pc * 1024;
+        const int ir = pc * 8 + prow;
+        const int wr = ir / (8 * TM), r = ir % (8 * TM);
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa) {
+            int row = m0 + wr * 16 * TM + qa * 8 * TM + r;
+            row = row < M ? row : M - 1;
+            sa[qa][i] = A + (long)row * lda + ((pch ^ (ir & 7)) << 3);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+        const int pc = wave + 8 * i;
+        lb[i] = pc * 1024;
+        const int ir = pc * 8 + prow;
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const uint16_t* wb = W;
+            int row;
+            if constexpr (DUAL) {
+                row = n0 + (ir >> 5) * 32 + (ir & 31);  // gate rows (qb 0) / the same up rows (qb 1)
+                if (qb) wb = W + up_off;
+            } else {
+                row = n0 + (ir >> 5) * 64 + qb * 32 + (ir & 31);
+            }
+            row = row < N ? row : N - 1;
+            sb[qb][i] = wb + (long)row * ldw + ((pch ^ (ir & 7)) << 3);
+        }
+    }
+#define PGMI_8P_LDS(off) ((__attribute__((address_space(3))) void*)(sm8 + (off)))
+    auto stageA = [&](int qa, int kt, int buf) {
+        kt = kt < kt1 ? kt : kt1 - 1;  // past the range: valid bytes into a buffer never read again
+        const int kel = kt * 64;
+        const int base = buf * TB + qa * HAB;
+#pragma unroll
+        for (int i = 0; i < GA; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(sa[qa][i] + kel), PGMI_8P_LDS(base + la[i]), 16, 0, 0);
+    };
+    auto stageB = [&](int qb, int kt, int buf) {
+        kt = kt < kt1 ? kt : kt1 - 1;
+        const int kel = kt * 64;
+        const int base = buf * TB + 2 * HAB + qb * HBB;
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(sb[qb][i] + kel), PGMI_8P_LDS(base + lb[i]), 16, 0, 0);
+    };
+#undef PGMI_8P_LDS
+
+    f32x4 acc[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    short8 fa[H][2], fb[2][2][2];             // fb[qb]: B0's fragments stay live from phase 1 to 4
+    const int sw = lane & 7;
+    const int arow = (wm * 8 * TM + (lane & 15)) * 128;  // + i * 16 rows
+    const int brow = (wn * 32 + (lane & 15)) * 128;      // + jj * 16 rows
+    auto readA = [&](int qa, int buf) {
+        const uint8_t* b = sm8 + buf * TB + qa * HAB + arow;
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                fa[i][kk] = *reinterpret_cast<const short8*>(b + i * 16 * 128 + (((kk * 4 + (lane >> 4)) ^ sw) << 4));
+    };
+    auto readB = [&](auto qb_c, int buf) {
+        constexpr int QB = decltype(qb_c)::value;
+        const uint8_t* b = sm8 + buf * TB + 2 * HAB + QB * HBB + brow;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                fb[QB][jj][kk] = *reinterpret_cast<const short8*>(b + jj * 16 * 128 + (((kk * 4 + (lane >> 4)) ^ sw) << 4));
+    };
+    auto mfmas = [&](auto qa_c, auto qb_c) {
+        constexpr int QA = decltype(qa_c)::value, QB = decltype(qb_c)::value;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < H; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+                    acc[QA * H + i][QB * 2 + jj] = mfma16(fa[i][kk], fb[QB][jj][kk], acc[QA * H + i][QB * 2 + jj]);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    static_assert(GA == GB, "one vmcnt for every half-tile");
+#define PGMI_8P_SB() __builtin_amdgcn_sched_barrier(0)
+#define PGMI_8P_TAIL(QAC, QBC, DO)                                      \
+    do {                                                                \
+        __builtin_amdgcn_s_barrier();                                   \
+        __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0) */            \
+        PGMI_8P_SB();                                                   \
+        __builtin_amdgcn_s_setprio(1);                                  \
+        if (DO) mfmas(QAC{}, QBC{});                                    \
+        __builtin_amdgcn_s_setprio(0);                                  \
+        PGMI_8P_SB();                                                   \
+        __builtin_amdgcn_s_barrier();                                   \
+    } while (0)
+    // the half-tile the next phase reads was issued four half-tiles (three phases) before this wait
+#define PGMI_8P_VMCNT() asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GA) : "memory")
+
+    // Phase p reads (buffer of its K-tile): 1: A0 B0, 2: B1, 3: A1, 4: none (A1 and the kept B0).
+    // Wave row 1 runs one barrier behind wave row 0 (one extra s_barrier up front, matched by wave
+    // row 0 after the loop), so on every SIMD one wave multiplies while its partner reads and
+    // stages.  Under that stagger a read of phase p is retired only by the barrier closing phase
+    // p + 1 for the leading row: a half is restaged two phases after its last read, in the order
+    // A0 B0 B1 A1, one half per phase; it is read one phase after the vmcnt + barrier retiring it.
+    // prologue: K-tile kt0 whole into buffer 0, kt0 + 1's A0 B0 into buffer 1
+    stageA(0, kt0, 0);
+    stageB(0, kt0, 0);
+    stageB(1, kt0, 0);
+    stageA(1, kt0, 0);
+    stageA(0, kt0 + 1, 1);
+    stageB(0, kt0 + 1, 1);
+    PGMI_8P_VMCNT();
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nkt; t += 2) {
+        const int T = kt0 + t;
+        const bool has1 = t + 1 < nkt;
+        // ---- K-tile T from buffer 0
+        readA(0, 0); readB(I0{}, 0); PGMI_8P_SB(); stageB(1, T + 1, 1); PGMI_8P_VMCNT(); PGMI_8P_TAIL(I0, I0, true);
+        readB(I1{}, 0); PGMI_8P_SB(); stageA(1, T + 1, 1); PGMI_8P_VMCNT();              PGMI_8P_TAIL(I0, I1, true);
+        readA(1, 0); PGMI_8P_SB(); stageA(0, T + 2, 0);                                  PGMI_8P_TAIL(I1, I1, true);
+        PGMI_8P_SB(); stageB(0, T + 2, 0); PGMI_8P_VMCNT();                              PGMI_8P_TAIL(I1, I0, true);
+        // ---- K-tile T + 1 from buffer 1 (absent past an odd tile count: the phases keep their
+        // barriers and stages, the MFMAs are skipped)
+        readA(0, 1); readB(I0{}, 1); PGMI_8P_SB(); stageB(1, T + 2, 0); PGMI_8P_VMCNT(); PGMI_8P_TAIL(I0, I0, has1);
+        readB(I1{}, 1); PGMI_8P_SB(); stageA(1, T + 2, 0); PGMI_8P_VMCNT();              PGMI_8P_TAIL(I0, I1, has1);
+        readA(1, 1); PGMI_8P_SB(); stageA(0, T + 3, 1);                                  PGMI_8P_TAIL(I1, I1, has1);
+        PGMI_8P_SB(); stageB(0, T + 3, 1); PGMI_8P_VMCNT();                              PGMI_8P_TAIL(I1, I0, has1);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // the lagging row's last barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail stages have landed
+#undef PGMI_8P_TAIL
+#undef PGMI_8P_VMCNT
+#undef PGMI_8P_SB
+
+    // ---- epilogue: acc[i][j] = rows m0 + wm*16*TM + 16 i, columns (qb = j / 2, jj = j % 2)
+    const int mb = m0 + wm * 16 * TM;
+    f32x4 a0[TM][2], a1[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            a0[i][jj] = acc[i][jj];
+            a1[i][jj] = acc[i][2 + jj];
+        }
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[i][j][r];
+                }
+            }
+    } else if constexpr (DUAL) {
+        epi_tile<EPI, TM, 2>(ea, M, N, mb, n0 + wn * 32, lane, a0, a1);
+    } else {
+        epi_tile<EPI, TM, 2>(ea, M, N, mb, n0 + wn * 64, lane, a0, a0);
+        epi_tile<EPI, TM, 2>(ea, M, N, mb, n0 + wn * 64 + 32, lane, a1, a1);
+    }
+}
+
 // Tile configurations (wave grid, per-wave MFMA tiles).  BM = WGM*TM*16, BN = WGN*TN*16.
 enum Cfg : int {
     C288x64 = 0,   // 6x1 waves, 3x4 tiles  (text rows: M = 288 = 18 x 16)
@@ -847,7 +1071,10 @@ enum Cfg : int {
     W352w = 33,    // 2x4 compute waves, TM 11, BN 128, 2 slots
     W128x128 = 34, // 2x4 compute waves, TM 4,  BN 128, 4 slots
     W128x64 = 35,  // 2x2 compute waves, TM 4,  BN 64,  5 slots
-    kNumCfg = 36,
+    // 8-phase (k_gemm_8p): 2x4 waves, BN 256 (dual: 128 gate + 128 up), two K-tile buffers
+    E256 = 36,     // TM 8: 256 rows
+    E192 = 37,     // TM 6: 192 rows
+    kNumCfg = 38,
 };
 static_assert(kNumCfg == kGemmCfgs, "launch.h kGemmCfgs");
 
@@ -888,8 +1115,8 @@ int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -936,8 +1163,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {2304, 16384, 2048, true, W288w, 1},    // text gate|up         308.9 us (was 377.4)
         {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (int i = 0; i < g_n_shape_plans; ++i) {
         const ShapePlan& o = g_shape_plans[i];
@@ -1084,6 +1311,42 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
 }
 
+// 8-phase launcher (K % 64 == 0); EPI < 0: partials only
+template <int TM, int EPI>
+static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
+                      const EpiArgs& ea, float* ws, int split, long up_off) {
+    constexpr bool DUAL = (EPI == EPI_GEGLU);
+    constexpr int BM = 32 * TM, BNO = DUAL ? 128 : 256;
+    constexpr size_t lds = (size_t)2 * (2 * 16 * TM * 128 + 2 * 128 * 128);
+    static_assert(lds <= 163840, "LDS exceeds 160 KiB");
+    constexpr int EK = EPI < 0 ? EPI_STORE : EPI;
+    const int nkt = K / 64;
+    const int per = (nkt + split - 1) / split;
+    const int n_mt = (M + BM - 1) / BM, n_nt = (N + BNO - 1) / BNO;
+    dim3 grid(n_mt * n_nt, split);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_8p<TM, EK, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_8p<TM, EK, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    if (EPI < 0 || split > 1) {
+        hipLaunchKernelGGL((k_gemm_8p<TM, EK, true>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
+                           up_off, n_mt);
+        if (EPI >= 0) {
+            long total4 = ((long)M * N + 3) / 4;
+            long blocks = (total4 + 255) / 256;
+            if (blocks > 4096) blocks = 4096;
+            hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
+        }
+    } else {
+        hipLaunchKernelGGL((k_gemm_8p<TM, EK, false>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
+                           up_off, n_mt);
+    }
+}
+
 template <int EPI>
 static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                         const EpiArgs& ea, float* ws, const Plan& p, long up_off) {
@@ -1120,6 +1383,8 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case W352w: launch_w<8, 2, 11, 2, 2, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case W128x128: launch_w<8, 2, 4, 2, 4, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case W128x64: launch_w<4, 2, 4, 2, 5, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case E256: launch_8p<8, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case E192: launch_8p<6, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         default: break;
     }
 #undef P_
@@ -1143,6 +1408,7 @@ static void launch_e(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
 int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K, Epi epi,
          const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows, bool defer) {
     Plan p = choose(M, N, K, epi == EPI_GEGLU);
+    if ((p.cfg == E256 || p.cfg == E192) && K % 64 != 0) p.cfg = P128w;  // the 8-phase kernel has no K tail
     if (p.split > 1 && (size_t)p.split * M * N * sizeof(float) > ws_bytes) p.split = 1;
     if (p.split > 1 && N % 4 != 0) p.split = 1;  // the split-K epilogue works on 4 outputs per thread
     const long up_off = (long)up_offset_rows * ldw;

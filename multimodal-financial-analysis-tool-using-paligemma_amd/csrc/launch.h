@@ -59,7 +59,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
 size_t gemm_ws_bytes(int M, int N, int K);
 void gemm_force_plan(int cfg, int split);  // cfg < 0: automatic
 int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split);  // cfg < 0: remove the override
-constexpr int kGemmCfgs = 36;              // tile configurations (kernels_gemm.hip Cfg)
+constexpr int kGemmCfgs = 38;              // tile configurations (kernels_gemm.hip Cfg)
 
 // ---------------------------------------------------------------- decode GEMV
 struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)

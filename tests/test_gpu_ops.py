@@ -240,3 +240,34 @@ def test_attention_forced_variant(eng, variant, B, Lq, Lk, H, Hkv, d, scale):
     finally:
         NN.check(eng.lib.pgmi_tune_attention(-1))
     assert rel_l2(np32(o), _attn_ref(q, k, v, scale)) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [36, 37])
+@pytest.mark.parametrize("M,N,K,epi,split", [
+    (1056, 512, 2048, "geglu", 1),     # 448 px gate|up shape (rows past 1056: clamped, never stored)
+    (300, 384, 1024, "store", 1),      # ragged M, N not a multiple of the tile
+    (520, 256, 2048, "res", 3),        # split-K partials + the fixed-order epilogue reduction
+    (256, 512, 192, "store", 1),       # 3 K-tiles: an odd tile count (the last iteration's second half idle)
+])
+def test_gemm_8phase(eng, cfg, M, N, K, epi, split):
+    """The 8-phase large-M GEMM (k_gemm_8p, plans E256 / E192) forced through the tuning hook."""
+    from pgmi import _native as NN
+    from pgmi._native import EPI
+    rng = np.random.default_rng(M + N + K + cfg)
+    A = rand(rng, M, K)
+    NN.check(eng.lib.pgmi_tune_gemm(cfg, split))
+    try:
+        if epi == "geglu":
+            Wg, Wu = rand(rng, N, K, scale=2 / np.sqrt(K)), rand(rng, N, K, scale=2 / np.sqrt(K))
+            got = _gemm(eng, bf(A), bf(np.concatenate([Wg, Wu])), 7, geglu=True)
+            ref = O.bf16(O.gelu_tanh(O.bf16(A @ Wg.T)) * O.bf16(A @ Wu.T))
+            tol = 5e-3
+        else:
+            Wt = rand(rng, N, K, scale=1 / np.sqrt(K))
+            r = rand(rng, M, N)
+            got = _gemm(eng, bf(A), bf(Wt), EPI[epi], res=bf(r))
+            ref = O.bf16(O.bf16(A @ Wt.T) + r) if epi == "res" else O.bf16(A @ Wt.T)
+            tol = 3e-3
+    finally:
+        NN.check(eng.lib.pgmi_tune_gemm(-1, 0))
+    assert rel_l2(got, ref) < tol

@@ -31,6 +31,8 @@ SHAPES = {  # name: (M, N, K, epi)
     # batched decode (configs[3]: 8 lock-step sequences) as GEMMs with 8 rows
     "b8_gateup": (8, 16384, 2048, 7), "b8_down": (8, 2048, 16384, 4), "b8_o": (8, 2048, 2048, 4),
     "b8_qkv": (8, 2560, 2048, 0),
+    # calibration against cdna_hip_programming.md's 256^2 8-phase template figures (square, plain store)
+    "sq4096": (4096, 4096, 4096, 0), "sq8192": (8192, 8192, 8192, 0),
 }
 
 

@@ -5,7 +5,8 @@ alone (pgmi_tune_gemm_shape) and the WHOLE tower / language model (graph-replaye
 split-K plans are charged with what their consumer (the residual + norm kernel) pays and every GEMM
 runs with the caches the layer loop leaves it.  Then the attention variants (pgmi_tune_attention).
 
-    python tools/probes/plan_sweep.py [--target vision|lm] [--batch 1] [--shapes ...] [--iters 20]
+    python tools/probes/plan_sweep.py [--target vision|lm] [--batch 1] [--px 224|448] [--shapes ...]
+                                      [--cfgs c,c,...] [--splits s,s,...] [--iters 20]
 """
 import argparse
 import os
@@ -56,20 +57,27 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--shapes", default=None)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--px", type=int, default=224, choices=[224, 448])
+    ap.add_argument("--cfgs", default=None, help="candidate tile configs (default: CFGS / CFGS_LM)")
+    ap.add_argument("--splits", default=None, help="candidate K splits (default: per shape)")
     a = ap.parse_args()
-    cfg = paligemma_3b_config(224)
-    eng = Engine(cfg, max_batch=a.batch, max_seq=320, max_kv=512)
+    if a.cfgs:
+        CFGS[:] = CFGS_LM[:] = [int(c) for c in a.cfgs.split(",")]
+    cfg = paligemma_3b_config(a.px)
+    n_img = (a.px // 14) ** 2
+    eng = Engine(cfg, max_batch=a.batch, max_seq=n_img + 64, max_kv=n_img + 256)
     eng.fill_synthetic(1234, init_policy)
     eng.prepare()
     g = torch.Generator(device="cuda").manual_seed(5)
-    px = (torch.rand((a.batch, 3, 224, 224), generator=g, device="cuda") * 2 - 1).contiguous()
+    px = (torch.rand((a.batch, 3, a.px, a.px), generator=g, device="cuda") * 2 - 1).contiguous()
     if a.target == "lm":
         from pgmi.synthetic import prompt_ids
-        L, M = 288, 288 * a.batch
-        ids = torch.from_numpy(prompt_ids(cfg["image_token_index"], 256, cfg["text_config"]["vocab_size"])).cuda()
+        L = n_img + 32
+        M = L * a.batch
+        ids = torch.from_numpy(prompt_ids(cfg["image_token_index"], n_img, cfg["text_config"]["vocab_size"])).cuda()
         ids = ids.expand(a.batch, -1).contiguous()
         feats = eng.project(eng.vision(px))
-        kv = eng.new_kv(a.batch, 512)
+        kv = eng.new_kv(a.batch, n_img + 256)
         args = ((kv, 0, torch.arange(L).expand(a.batch, L)), dict(ids=ids, image_feats=feats, logits_rows=2))
         shapes = {"qkv": (M, 2560, 2048, 0, [1, 2, 4]), "o": (M, 2048, 2048, 0, [1, 2, 4, 8]),
                   "gateup": (M, 16384, 2048, 1, [1]), "down": (M, 2048, 16384, 0, [4, 8, 12, 16])}
@@ -78,6 +86,8 @@ def main():
         print(f"lm forward (current plans): {base:.1f} us", flush=True)
         for name in (a.shapes or "qkv,o,gateup,down").split(","):
             Mm, Nn, K, dual, splits = shapes[name]
+            if a.splits and not dual:
+                splits = [int(x) for x in a.splits.split(",")]
             rows = []
             for c in CFGS_LM:
                 for sp in splits:
@@ -90,7 +100,7 @@ def main():
             print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (d {e:.2g})" for t, c, sp, e in rows[:8]),
                   flush=True)
         return
-    M = 256 * a.batch
+    M = n_img * a.batch
     shapes = {"qkv": (M, 3456, 1152, [1, 2]), "out": (M, 1152, 1152, [1, 2, 3, 4, 6]),
               "fc1": (M, 4304, 1152, [1, 2]), "fc2": (M, 1152, 4304, [1, 2, 3, 4, 6, 8, 12, 16])}
     ref = eng.vision(px).clone()
@@ -107,6 +117,8 @@ def main():
             print("attn: " + ", ".join(f"v{v}: {t:.1f}" for t, v in rows), flush=True)
             continue
         Mm, Nn, K, splits = shapes[name]
+        if a.splits:
+            splits = [int(x) for x in a.splits.split(",")]
         rows = []
         for c in CFGS:
             for sp in splits:

@@ -1146,8 +1146,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {256, 2048, 1152, false, P32x64s4, 1},  // multimodal projector   7.6 us
         {1056, 2560, 2048, false, W128x128, 1}, // 448 px text q|k|v     21.3 us (P96x64s3 24.0 in the same sweep)
         {1056, 2048, 2048, false, W128x128, 1}, // 448 px text o_proj    19.5 us (P96x64s3 23.9)
-        {1056, 16384, 2048, true, W352w, 1},    // 448 px gate|up       153.8 us (was 180.9 cold)
-        {1056, 2048, 16384, false, W288w, 4},   // 448 px down           79.1 us (was 99.5 cold)
+        {1056, 16384, 2048, true, E192, 1},     // 448 px gate|up       135.5 us (W352w 149.8); in situ LM 5688 -> 5538 us
+        {1056, 2048, 16384, false, E192, 4},    // 448 px down          (W288w split 4 79.1 us); in situ 5688 -> 5539 us
         {1024, 3456, 1152, false, W128x128, 1}, // 448 px vision q|k|v   18.3 us (was 24.6)
         {1024, 1152, 1152, false, P96x64s4, 1}, // 448 px vision out     10.6 us (P32x64s4 13.7)
         {1024, 4304, 1152, false, W288w, 1},    // 448 px vision fc1     25.1 us (exp/rcp GELU; was 29.5)
@@ -1160,7 +1160,7 @@ static Plan choose(int M, int N, int K, bool dual) {
         {2048, 2048, 1152, false, W128x128, 1}, // projector             19.1 us (was 23.8)
         {2304, 2560, 2048, false, W288w, 1},    // text q|k|v            32.8 us (was 48.3)
         {2304, 2048, 2048, false, W288n, 1},    // text o_proj           35.4 us (was 62.1)
-        {2304, 16384, 2048, true, W288w, 1},    // text gate|up         308.9 us (was 377.4)
+        {2304, 16384, 2048, true, E256, 1},     // text gate|up         261.8 us (W288w 301.8); in situ LM 10064 -> 9435 us
         {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)
     };
     static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192};

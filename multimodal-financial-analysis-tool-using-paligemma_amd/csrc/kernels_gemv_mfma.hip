@@ -14,7 +14,7 @@
 //     each of its 16 rows (non-temporal);
 //   - A operand (activations, B x K bf16): the wave's K slice held in registers, staged through
 //     LDS (row stride K + 8: conflict-free 16-B reads) with the RMSNorm (modeling_gemma.py:114-120)
-//     or the flash-decoding combine (o_proj) fused in, or read from global (down_proj's input);
+//     fused in, or read from global (o_proj's and down_proj's inputs);
 //   - epilogues and rounding points exactly as gemv_body.h (RoPE + KV append, GeGLU, residual,
 //     fp32 logits + per-workgroup first-max argmax partials).
 #include "gemv_body.h"
@@ -22,35 +22,6 @@
 namespace pgmi {
 
 constexpr int MF_MAXB = 16;
-
-// flash-decoding combine of k_attn_decode's partials into xs rows (stride ld), fixed chunk order
-// (the GV_ORES prologue of gemv_body.h, restated for the padded LDS image)
-__device__ void mf_stage_ores(const GemvArgs& a, int K, uint16_t* xs, int ld) {
-    const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
-    for (int e8 = threadIdx.x; e8 < a.nb * K / 8; e8 += blockDim.x) {
-        const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
-        const int h = e >> 8;
-        const float* pb = a.part + (long)b * a.max_chunks * kAttnPartStride + h * 256 + (e & 255);
-        const float* sp = a.part + (long)b * a.max_chunks * kAttnPartStride + 16 * 256 + h;
-        float M = -INFINITY, S = 0.f, o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = 0.f;
-        for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
-        for (int c = 0; c < nch; ++c) {
-            const float w = expf(sp[(long)c * kAttnPartStride] - M);
-            S += w * sp[(long)c * kAttnPartStride + 16];
-            const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
-            const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
-        }
-        u16x8 ob;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(o[j] / S);
-        *reinterpret_cast<u16x8*>(xs + b * ld + e) = ob;
-        if (a.o_out && blockIdx.x == 0) *reinterpret_cast<u16x8*>(a.o_out + (long)b * K + e) = ob;
-    }
-}
 
 // RMSNorm'd (or plain) activation rows into xs (stride ld).  Every row's chunks are loaded
 // before any is reduced (one round trip for the whole [nb][K] block, not one per row).
@@ -134,6 +105,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     // n < 8 and d + 128 in lane n + 8 (the partner value is one lane swap away in the C map), so the
     // 2,560 rows make 160 groups
     static_assert(MODE != GV_QKV || NR == 1, "q|k|v: one weight row per lane");
+    static_assert(MODE != GV_ORES, "o_proj at B >= 3: k_attn_combine, then GV_RES");
     auto row_of = [&](int u, int j) -> long {
         if constexpr (MODE == GV_QKV) {
             const int grp_ = u >> 4, nn = u & 15;
@@ -172,8 +144,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     // ---- activations: this wave's K slice, MFMA A layout (row b = lane & 15)
     short8 xf[NKB][4];
     if constexpr (STAGE) {
-        if constexpr (MODE == GV_ORES) mf_stage_ores(a, K, mfs, ld);
-        else mf_stage_rows(a, K, mfs, ld, red);
+        mf_stage_rows(a, K, mfs, ld, red);
         __syncthreads();
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
@@ -265,8 +236,6 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
             if constexpr (MODE == GV_RES) {
                 if (KS > 1) ws[((long)ks * a.nb + b) * a.n_units + u] = acc[0][r];
                 else a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
-            } else if constexpr (MODE == GV_ORES) {
-                a.out[(long)b * a.n_units + u] = f2bf(rbf(acc[0][r]) + bf2f(a.out[(long)b * a.n_units + u]));
             } else if constexpr (MODE == GV_GEGLU) {
                 const float gg = rbf(gelu_tanh(rbf(acc[0][r])));
                 a.out[(long)b * a.I + u] = f2bf(gg * rbf(acc[1][r]));
@@ -475,7 +444,7 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
 }
 
 // flash-decoding combine of k_attn_decode's partials -> o (bf16 [nb][G*256]), one thread per
-// 8 outputs, chunk records in a fixed order (the GV_ORES prologue, once per output)
+// 8 outputs, chunk records in a fixed order (gemv_body.h's GV_ORES prologue, once per output)
 __global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __restrict__ o, int K) {
     const int e8 = blockIdx.x * 256 + threadIdx.x;
     if (e8 >= a.nb * K / 8) return;

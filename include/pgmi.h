@@ -211,7 +211,9 @@ int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split);
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
  * LDS-resident scores, 7 = one pass with K/V loaded once and scores in registers (head_dim 72, <= 256 keys),
  * 8 = the same 16-row kernel with every K/V load issued up front (head_dim 256, <= 320 keys), RK = K/V-tiled two-pass kernel with R row groups and K key-split groups
- * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); -1 restores the measured choice. */
+ * per workgroup (41, 42, 21, 22; 44, 24 for head_dim 72); 9 = one pass with the keys split over workgroups
+ * (online softmax, fp32 partials merged by a combine kernel), 91 / 92 / 94 = the same with 1 / 2 / 4 key
+ * ranges; -1 restores the measured choice. */
 int pgmi_tune_attention(int variant);
 
 /* Nucleus sampling, inference.py:15-24 (_sample_top_p) with inference.py:65's

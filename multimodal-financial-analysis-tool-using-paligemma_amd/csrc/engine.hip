@@ -700,6 +700,7 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
         a.v = x->vQKV + 2 * D; a.v_b_stride = a.q_b_stride; a.v_row_stride = 3 * D; a.v_head_stride = 72;
         a.o = x->vAO; a.o_b_stride = (long)N * D; a.o_row_stride = D; a.o_head_stride = 72;
         a.Lq = N; a.Lk = N; a.G = 1; a.n_kv = c.v_heads; a.B = B; a.scale = scale;
+        a.ws = x->ws; a.ws_floats = (long)(x->ws_bytes / sizeof(float));
         attention_prefill(s, 72, a);
         EpiArgs o{};
         o.bias = VL(x, i, "self_attn.out_proj.bias");
@@ -832,6 +833,7 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         a.o = x->AO; a.o_b_stride = (long)L * H; a.o_row_stride = H; a.o_head_stride = HD;
         a.Lq = L; a.Lk = kv_start + L; a.G = NH / NKV; a.n_kv = NKV; a.B = B;
         a.scale = 1.0f / std::sqrt((float)HD);  // / math.sqrt(head_dim) (:266): exact power of two
+        a.ws = x->ws; a.ws_floats = (long)(x->ws_bytes / sizeof(float));
         if (last_only && i + 1 == c.t_layers) {
             // logits_rows == 2, last layer: the K/V rows of every token are written above (the cache
             // the decode loop reads); the rest of the layer feeds only the final hidden state, and the
@@ -1215,7 +1217,7 @@ int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split) {
 }
 
 int pgmi_tune_attention(int variant) {
-    static const int ok[] = {-1, 0, 7, 8, 41, 42, 21, 22, 44, 24};
+    static const int ok[] = {-1, 0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94};
     for (int v : ok)
         if (v == variant) {
             attention_force_variant(variant);
@@ -1288,6 +1290,7 @@ int pgmi_op_attention(pgmi_ctx* x, const void* q, const void* k, const void* v, 
     a.v = reinterpret_cast<const uint16_t*>(v); a.v_b_stride = a.k_b_stride; a.v_row_stride = Hkv * hd; a.v_head_stride = hd;
     a.o = reinterpret_cast<uint16_t*>(o); a.o_b_stride = a.q_b_stride; a.o_row_stride = H * hd; a.o_head_stride = hd;
     a.Lq = Lq; a.Lk = Lk; a.G = H / Hkv; a.n_kv = Hkv; a.B = B; a.scale = scale;
+    a.ws = x->ws; a.ws_floats = (long)(x->ws_bytes / sizeof(float));
     attention_prefill((hipStream_t)stream, hd, a);
     LAUNCHCHK();
     return 0;

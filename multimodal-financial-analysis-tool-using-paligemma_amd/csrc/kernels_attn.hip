@@ -18,6 +18,7 @@
 #include "common.h"
 #include "launch.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace pgmi {
@@ -784,6 +785,362 @@ __global__ void __launch_bounds__(256) k_attn_short(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- prefill, one pass, keys split over workgroups
+// For the long prefills (Gemma and SigLIP at 448 px, L ~ 1,056): k_attn_fa reads every key's K twice
+// and V once per 64 query rows, and with all keys in one workgroup only ~130 workgroups exist, each
+// pulling ~1.6 MB through its CU (~30 GB/s per CU: the kernel is bound by that intake, MFMA busy
+// < 0.1).  Here a workgroup owns QB = NW x 16 query rows (MQA: the G heads of a KV head are rows of
+// the same tiles) and one of `ns` contiguous key ranges; K and V reach LDS by LDS-DMA into an
+// ST-slot ring filled by LW loader waves (counted vmcnt, one raw s_barrier per 32-key tile); the NW
+// compute waves run S^T = K Q^T, an online softmax and P.V on MFMA.  Each workgroup writes its
+// unnormalised O (fp32) and its per-row (max, sum) to scratch; k_attn_fs_combine merges the key
+// ranges in a fixed order (ns == 1: the workgroup normalises and stores bf16 itself).
+// Rounding: s = bf16(bf16(k.q) * scale) as the reference; p is rounded to bf16 as exp(s - m) with m
+// the workgroup's running row max (deferred: raised only when a tile's max passes it by kFsDefer,
+// e <= e^8 in between) and normalised in fp32 at the end, where the reference rounds the globally
+// normalised p -- the flash-decoding deviation of the decode step.
+// LDS images (rows of CR 16-B chunks): K chunk c of key row r at chunk c ^ (r & 15) (conflict-free
+// ds_read_b128 of 16 rows x one 16-B k slice); V chunk c at chunk c ^ ((r & 7) << 1) (the
+// ds_read_b64_tr_b16 reads of 8 rows x 32 B per half-wave hit 8 distinct 32-B bank groups).  The
+// swizzle is applied to each lane's SOURCE address (the LDS-DMA destination is lane-linear); chunks
+// past the head dim (HD 72) load a copy of chunk 0 (finite; multiplied by Q's zeroed k range, or
+// feeding output columns that are never stored).
+template <int HD>
+struct FSInfo {
+    static constexpr int KS = (HD + 31) / 32;        // 32-deep k-steps of K.Q
+    static constexpr int CT = (HD + 15) / 16;        // 16-wide output tiles of P.V
+    static constexpr int CH = (HD + 7) / 8;          // 16-B chunks of a head row in HBM
+    static constexpr int CR = HD <= 128 ? 16 : 32;   // 16-B chunks of an LDS row
+    static constexpr int ROWB = CR * 16;
+    static constexpr int TILEB = 32 * ROWB;          // one 32-key K (or V) image
+    static constexpr int SLOTB = 2 * TILEB;          // ring slot: K image, then V image
+    static constexpr int PCS = SLOTB / 1024;         // 1-KiB LDS-DMA pieces per slot
+    static_assert(CR >= 4 * KS && CR >= 2 * CT && CR >= 16, "LDS row holds every k-step and tile");
+};
+constexpr float kFsDefer = 8.0f;
+
+template <int G, int NMAX>
+__device__ __forceinline__ void fs_vm_wait(int n) {  // s_waitcnt vmcnt(G * min(n, NMAX))
+    if constexpr (NMAX >= 1) {
+        if (n >= NMAX) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * NMAX) : "memory");
+            return;
+        }
+        fs_vm_wait<G, NMAX - 1>(n);
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+// grid (row blocks, n_kv * ns, B); key range sp = blockIdx.y % ns covers tiles [sp * tps, (sp + 1) * tps)
+// P2: scale is a power of two (Gemma: 1/16), so bf16(bf16(x) * scale) = bf16(x) * scale (one rounding)
+template <int HD, int NW, int LW, int ST, bool P2>
+__global__ void __launch_bounds__(64 * (NW + LW), 1) k_attn_fs(AttnArgs a, int ns, int tps) {
+    using I = FSInfo<HD>;
+    constexpr int KS = I::KS, CT = I::CT, CH = I::CH, CR = I::CR, ROWB = I::ROWB, TILEB = I::TILEB;
+    constexpr int SLOTB = I::SLOTB, PCS = I::PCS, GPW = PCS / LW;
+    constexpr int QB = NW * 16;
+    static_assert(PCS % LW == 0, "whole pieces per loader wave");
+    extern __shared__ __attribute__((aligned(16))) uint8_t fs_sm[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.z, kvh = blockIdx.y / ns, sp = blockIdx.y % ns;
+    const int nt = (a.Lk + 31) / 32;
+    const int t0 = sp * tps;
+    const int t1 = t0 + tps < nt ? t0 + tps : nt;
+    const int ntl = t1 > t0 ? t1 - t0 : 0;
+    const uint16_t* kbase = a.k + b * a.k_b_stride + kvh * a.k_head_stride;
+    const uint16_t* vbase = a.v + b * a.v_b_stride + kvh * a.v_head_stride;
+
+    if (wave >= NW) {
+        // ---------------- loader wave: pieces lw, lw + LW, ... of every slot
+        const int lw = wave - NW;
+        constexpr int RPP = 1024 / ROWB;  // key rows per piece
+        int loff[GPW], prow[GPW], pch[GPW];
+        bool pv[GPW];
+#pragma unroll
+        for (int i = 0; i < GPW; ++i) {
+            const int p = lw + LW * i;
+            pv[i] = p >= PCS / 2;
+            const int q = pv[i] ? p - PCS / 2 : p;
+            loff[i] = (pv[i] ? TILEB : 0) + q * 1024;
+            const int r = q * RPP + lane / CR, pos = lane % CR;
+            const int c = pv[i] ? pos ^ ((r & 7) << 1) : pos ^ (r & 15);
+            pch[i] = c < CH ? c : 0;
+            prow[i] = r;
+        }
+        auto issue = [&](int t, int slot) {
+#pragma unroll
+            for (int i = 0; i < GPW; ++i) {
+                int key = t * 32 + prow[i];
+                key = key < a.Lk ? key : a.Lk - 1;  // rows past the keys: a valid row, masked (s = -inf)
+                const uint16_t* src =
+                    (pv[i] ? vbase + (long)key * a.v_row_stride : kbase + (long)key * a.k_row_stride) + pch[i] * 8;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 (__attribute__((address_space(3))) void*)(fs_sm + slot * SLOTB + loff[i]),
+                                                 16, 0, 0);
+            }
+        };
+#pragma unroll
+        for (int sI = 0; sI < ST - 1; ++sI)
+            if (sI < ntl) issue(t0 + sI, sI);
+        int slot_next = ST - 1;  // slot of tile it + ST - 1
+        for (int it = 0; it < ntl; ++it) {
+            // barrier it: tiles it and it + 1 landed (the compute waves multiply K of it + 1 while
+            // they finish tile it); the slot refilled after it held tile it - 1, done with at barrier it
+            const int issued = ntl < it + ST - 1 ? ntl : it + ST - 1;
+            const int need = it + 1 < ntl ? it + 1 : ntl - 1;
+            fs_vm_wait<GPW, ST - 3>(issued - need - 1);
+            __builtin_amdgcn_s_barrier();
+            if (it + ST - 1 < ntl) issue(t0 + it + ST - 1, slot_next);
+            slot_next = slot_next + 1 == ST ? 0 : slot_next + 1;
+        }
+        return;
+    }
+
+    // ---------------- compute wave: query rows rbase + li (16 per wave)
+    const int g = lane >> 4, li = lane & 15;
+    const int nrows = a.Lq * a.G;
+    const int rbase = blockIdx.x * QB + wave * 16;
+    short8 qf[KS];
+    {
+        int qi = rbase + li;
+        qi = qi < nrows ? qi : nrows - 1;  // rows past the end: a valid row, never stored
+        const int qpos = qi / a.G, qhead = kvh * a.G + qi % a.G;
+        const uint16_t* qrow = a.q + b * a.q_b_stride + (long)qpos * a.q_row_stride + qhead * a.q_head_stride;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) qf[kk] = load_frag<HD>(qrow, true, kk, lane);
+    }
+    f32x4 o[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // row li's running (deferred) max -- finite from the start, so exp(s - m) of a masked key (s = -inf)
+    // is 0 and the first tile's rescale factor exp(m - tm) is 0 without a special case -- and this
+    // lane's share of the row sum
+    float m = -1e30f, l = 0.f;
+    // P.V operand: lane reads rows vr0 (lo) and vr0 + 16 (hi), columns 16c + 4 (li & 3) .. + 3
+    const int vr0 = 4 * g + (li >> 2);
+    const int vsw = (vr0 & 7) << 1;
+    // S^T = K Q^T of the tile in `sl`: lane holds keys 16 kt + 4 g + j of query li; even / odd
+    // k-steps accumulate in two chains
+    auto scores = [&](int sl, f32x4 (&ac)[2][2]) {
+        const uint8_t* kb = fs_sm + sl * SLOTB;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) ac[kt][0] = ac[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                const int r = kt * 16 + li;
+                const short8 kf = *reinterpret_cast<const short8*>(kb + r * ROWB + (((kk * 4 + g) ^ (r & 15)) << 4));
+                ac[kt][kk & 1] = mfma16(kf, qf[kk], ac[kt][kk & 1]);
+            }
+    };
+    // s = bf16(bf16(k.q) * scale), keys past Lk masked (the last tile only: wave-uniform branch);
+    // returns the tile's max of row li
+    auto finish = [&](int t, const f32x4 (&ac)[2][2], float (&sv)[2][4]) -> float {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x = rbf(ac[kt][0][j] + ac[kt][1][j]);
+                sv[kt][j] = P2 ? x * a.scale : rbf(x * a.scale);
+            }
+        if (t * 32 + 32 > a.Lk) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (t * 32 + kt * 16 + 4 * g + j >= a.Lk) sv[kt][j] = -INFINITY;
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sv[kt][j]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        return fmaxf(mx, __shfl_xor(mx, 32, 64));
+    };
+    // one tile ahead: iteration it multiplies K of tile it + 1 while it runs the softmax and P.V of
+    // tile it (the two are independent, so the MFMAs of one overlap the VALU of the other)
+    float s[2][4], tm = -INFINITY;
+    if (ntl > 0) {
+        __builtin_amdgcn_s_barrier();  // barrier 0: tiles 0 and 1 landed
+        f32x4 ac[2][2];
+        scores(0, ac);
+        tm = finish(t0, ac, s);
+    }
+    int slot = 0;
+    for (int it = 0; it < ntl; ++it) {
+        if (it > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the slot refilled next is done
+            __builtin_amdgcn_s_barrier();                         // tiles it and it + 1 in the ring
+        }
+        const int nslot = slot + 1 == ST ? 0 : slot + 1;
+        f32x4 acn[2][2];
+        scores(nslot, acn);  // tile it + 1 (past the last tile: stale LDS, never used)
+        // deferred running max: raised (and O, l rescaled) only when a row's tile max passes it by
+        // kFsDefer; wave-uniform branch
+        if (__ballot(tm > m + kFsDefer)) {
+            const float mn = fmaxf(m, tm);
+            const float alpha = fa_exp(m - mn);
+            l *= alpha;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float ar = __shfl(alpha, 4 * g + r, 64);  // O rows are queries 4g + r
+#pragma unroll
+                for (int c = 0; c < CT; ++c) o[c][r] *= ar;
+            }
+            m = mn;
+        }
+        short8 pa;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float e = fa_exp(s[kt][j] - m);  // masked: exp(-inf) = 0
+                l += e;
+                pa[kt * 4 + j] = (short)f2bf(e);
+            }
+        const uint8_t* vb = fs_sm + slot * SLOTB + TILEB;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int cidx = 2 * c + ((li & 3) >> 1);
+            const uint8_t* pl = vb + vr0 * ROWB + ((cidx ^ vsw) << 4) + (li & 1) * 8;
+            const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)pl);
+            const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(pl + 16 * ROWB));
+            const short8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[c] = mfma16(pa, vv, o[c]);
+        }
+        tm = finish(t0 + it + 1, acn, s);
+        slot = nslot;
+    }
+    // row sums: the 4 lane groups of query li, in a fixed order
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (ns == 1) {
+        const float inv = 1.0f / l;
+        uint16_t* orow[4];
+        attn_out_rows(a, b, kvh, rbase + 4 * g, nrows, orow);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float ir = __shfl(inv, 4 * g + r, 64);
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                const int d = c * 16 + li;
+                if (d < HD && orow[r]) orow[r][d] = f2bf(o[c][r] * ir);
+            }
+        }
+        return;
+    }
+    // key-split partials: O rows [(b, kvh, sp)][row][HD] fp32, then (m, l) pairs
+    const long rec = ((long)(b * a.n_kv + kvh) * ns + sp) * nrows;
+    float* part = a.ws;
+    float* ml = a.ws + (long)a.B * a.n_kv * ns * nrows * HD;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = rbase + 4 * g + r;
+        if (row >= nrows) continue;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int d = c * 16 + li;
+            if (d < HD) part[(rec + row) * HD + d] = o[c][r];
+        }
+    }
+    if (g == 0 && rbase + li < nrows) {
+        ml[(rec + rbase + li) * 2 + 0] = m;
+        ml[(rec + rbase + li) * 2 + 1] = l;
+    }
+}
+
+// merge the key ranges of k_attn_fs in range order: O = sum_sp w_sp O_sp / sum_sp w_sp l_sp,
+// w_sp = exp(m_sp - max m); one thread per 8 output columns of a row
+template <int HD>
+__global__ void __launch_bounds__(256) k_attn_fs_combine(AttnArgs a, int ns) {
+    constexpr int C8 = HD / 8;
+    const int nrows = a.Lq * a.G;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long)a.B * a.n_kv * nrows * C8) return;
+    const int c8 = (int)(e % C8);
+    long rr = e / C8;
+    const int row = (int)(rr % nrows);
+    rr /= nrows;
+    const int kvh = (int)(rr % a.n_kv), b = (int)(rr / a.n_kv);
+    const float* ml = a.ws + (long)a.B * a.n_kv * ns * nrows * HD;
+    const long rec0 = (long)(b * a.n_kv + kvh) * ns * nrows + row;
+    float M = -INFINITY;
+    for (int q = 0; q < ns; ++q) M = fmaxf(M, ml[(rec0 + (long)q * nrows) * 2]);
+    float L = 0.f, acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int q = 0; q < ns; ++q) {
+        const long r = rec0 + (long)q * nrows;
+        const float mq = ml[r * 2], lq = ml[r * 2 + 1];
+        const float w = mq == -INFINITY ? 0.f : fa_exp(mq - M);  // an empty range: O = 0, l = 0
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(a.ws + r * HD + c8 * 8);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(a.ws + r * HD + c8 * 8 + 4);
+        L += w * lq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[j] += w * x0[j]; acc[4 + j] += w * x1[j]; }
+    }
+    const float inv = 1.0f / L;
+    u16x8 ob;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(acc[j] * inv);
+    const int pos = row / a.G, head = kvh * a.G + row % a.G;
+    *reinterpret_cast<u16x8*>(a.o + b * a.o_b_stride + (long)pos * a.o_row_stride + head * a.o_head_stride + c8 * 8) = ob;
+}
+
+// key ranges for k_attn_fs.  A workgroup takes the whole LDS (one per CU), so a grid past 256
+// workgroups runs in two rounds: split the keys (2, 4, ...) only while the grid stays within one
+// round and every range keeps >= 16 tiles (shorter ranges lose more to the combine than they gain);
+// scratch for the partials or the split is dropped
+static int fs_splits(const AttnArgs& a, int HD, int QB, int want) {
+    const int nrows = a.Lq * a.G, nt = (a.Lk + 31) / 32;
+    const long blocks = (long)(nrows + QB - 1) / QB * a.n_kv * a.B;
+    int ns = 1;
+    if (want > 0) ns = want;
+    else
+        while (blocks * ns * 2 <= 256 && nt / (ns * 2) >= 16) ns *= 2;
+    if (ns > nt) ns = nt;
+    while (ns > 1 && (!a.ws || (long)a.B * a.n_kv * ns * nrows * (HD + 2) > a.ws_floats)) ns >>= 1;
+    return ns < 1 ? 1 : ns;
+}
+
+template <int HD, int NW, int LW, int ST, bool P2>
+static void launch_fs_t(hipStream_t s, const AttnArgs& a, int ns, int tps, dim3 grid) {
+    constexpr size_t lds = (size_t)ST * FSInfo<HD>::SLOTB;
+    static_assert(lds <= 160 * 1024, "LDS");
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_fs<HD, NW, LW, ST, P2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_attn_fs<HD, NW, LW, ST, P2>), grid, dim3(64 * (NW + LW)), lds, s, a, ns, tps);
+}
+
+template <int HD>
+static void launch_fs(hipStream_t s, const AttnArgs& a, int want_ns) {
+    // head dim 256: 4 compute waves (their registers fit 2 waves per SIMD with the loaders, not 3) and a
+    // 5-slot ring (160 KiB); head dim 72: 8 compute waves, 8 slots
+    constexpr int NW = HD == 256 ? 4 : 8, LW = 4, ST = HD == 256 ? 5 : 8;
+    const int nrows = a.Lq * a.G, nt = (a.Lk + 31) / 32;
+    int ns = fs_splits(a, HD, NW * 16, want_ns);
+    const int tps = (nt + ns - 1) / ns;
+    ns = (nt + tps - 1) / tps;  // no empty range
+    dim3 grid((nrows + NW * 16 - 1) / (NW * 16), a.n_kv * ns, a.B);
+    int e2 = 0;
+    const bool p2 = std::frexp(a.scale, &e2) == 0.5f;
+    if (p2) launch_fs_t<HD, NW, LW, ST, true>(s, a, ns, tps, grid);
+    else launch_fs_t<HD, NW, LW, ST, false>(s, a, ns, tps, grid);
+    if (ns > 1) {
+        const long n8 = (long)a.B * a.n_kv * nrows * (HD / 8);
+        hipLaunchKernelGGL(k_attn_fs_combine<HD>, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, a, ns);
+    }
+}
+
 template <int HD, int RG, int KSPL>
 static void launch_fa(hipStream_t s, const AttnArgs& a) {
     using I = FAInfo<HD>;
@@ -835,10 +1192,16 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         //   SigLIP 448 (1024 x 16):            16-row 153.5 | RG4xKSPL4 32.4 | RG4xKSPL2 36.0
         //   Gemma 224 (288 x 8 heads, MQA):    16-row 21.9 | RG4xKSPL2 26.1 | RG2xKSPL2 26.4
         //   Gemma 448 (1056 x 8):              16-row 159.5 | RG4xKSPL2 61.3 | RG2xKSPL2 122.7
-        // few rows -> the 16-row kernel (Gemma) or more, smaller workgroups (SigLIP)
-        const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
-        if (head_dim == 256) v = rows <= 4096 ? (a.Lk <= 320 ? 8 : 0) : 42;
-        else v = a.Lk <= 256 ? 7 : rows <= 8192 ? 24 : 44;
+        // round 3 (same probe, graph-replayed): the one-pass key-split kernel k_attn_fs (variant 9)
+        //   Gemma 224 12.2 (full_pre 15.1) | Gemma 448 31.7 (tiled RG4xKSPL2 52.5) | SigLIP 448 24.4 (31.8);
+        //   SigLIP 224 stays on k_attn_short (6.7 against 10.6)
+        v = head_dim == 256 ? 9 : a.Lk <= 256 ? 7 : 9;
+    }
+    if (v == 9 || v == 91 || v == 92 || v == 94) {  // one pass, keys split over workgroups (auto / 1 / 2 / 4 ranges)
+        const int want = v == 9 ? 0 : v - 90;
+        if (head_dim == 256) launch_fs<256>(s, a, want);
+        else launch_fs<72>(s, a, want);
+        return;
     }
     if (v == 7 && head_dim == 72 && a.Lk <= 256) {
         dim3 grid((a.Lq * a.G + 15) / 16, a.n_kv, a.B);

@@ -116,6 +116,8 @@ struct AttnArgs {
     int n_kv;      // kv heads
     int B;
     float scale;   // s = bf16(bf16(q.k) * scale)
+    float* ws;     // prefill: fp32 scratch for key-split partials (nullptr: no key split)
+    long ws_floats;
 };
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
 // decode: Lq == 1, rows = the G heads; keys split over chunks; kv length from StepState (+1)

@@ -214,7 +214,7 @@ def test_argmax_rows(eng, rows, V):
         assert torch.equal(got.cpu(), y[1:].view(rows, V).argmax(-1))
 
 
-@pytest.mark.parametrize("variant", [0, 7, 8, 41, 42, 21, 22, 44, 24])
+@pytest.mark.parametrize("variant", [0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94])
 @pytest.mark.parametrize("B,Lq,Lk,H,Hkv,d,scale", [
     (1, 256, 256, 16, 16, 72, 72 ** -0.5),     # SigLIP 224
     (3, 17, 5, 16, 16, 72, 72 ** -0.5),        # fewer keys than one tile
@@ -223,6 +223,9 @@ def test_argmax_rows(eng, rows, V):
     (1, 288, 288, 8, 1, 256, 1 / 16),          # Gemma prefill (MQA)
     (2, 33, 70, 8, 1, 256, 1 / 16),            # ragged, keys beyond queries (cache)
     (1, 288, 576, 8, 1, 256, 1 / 16),          # the ablation's step-0 re-feed: 2L keys
+    (1, 1056, 1056, 8, 1, 256, 1 / 16),        # Gemma 448 prefill
+    (1, 1024, 1024, 16, 16, 72, 72 ** -0.5),   # SigLIP 448
+    (2, 300, 1000, 8, 1, 256, 1 / 16),         # ragged key ranges (a last range shorter than the others)
 ])
 def test_attention_forced_variant(eng, variant, B, Lq, Lk, H, Hkv, d, scale):
     """Every prefill attention kernel the tuning hook (pgmi_tune_attention) can force, against the

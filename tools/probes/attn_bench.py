@@ -1,6 +1,7 @@
 """Probe: prefill attention kernel time at the PaliGemma shapes (SigLIP / Gemma, 224 / 448 px)
 for every variant of pgmi_tune_attention (0 = 16-row kernel, RK = tiled with R row groups and
-K key splits, 100 * PD + RK = the same with a register prefetch of PD tiles, -1 = the default choice), plus a rel-L2 check against a torch fp32 attention with
+K key splits, 7 / 8 = the one-pass short-range kernels, 9 / 9N = the one-pass key-split kernel
+(auto / N key ranges), -1 = the default choice), plus a rel-L2 check against a torch fp32 attention with
 the reference's rounding points.
     python tools/probes/attn_bench.py [variants...]
 """
@@ -20,12 +21,14 @@ eng.fill_synthetic(1, W.init_policy)
 eng.prepare()
 shapes = [("siglip224", 256, 16, 16, 72), ("siglip448", 1024, 16, 16, 72),
           ("gemma224", 288, 8, 1, 256), ("gemma448", 1056, 8, 1, 256)]
+if os.environ.get("ATTN_SHAPES"):
+    shapes = [sh for sh in shapes if sh[0] in os.environ["ATTN_SHAPES"].split(",")]
 torch.manual_seed(0)
-variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 8, 41, 42, 21, 22, 44, 24, 91, 92, 94]
+variants = [int(v) for v in sys.argv[1:]] or [-1, 7, 8, 42, 44, 24, 9, 91, 92, 94]
 for var, (name, L, H, Hkv, d) in [(v, sh) for sh in shapes for v in variants]:
     if var % 100 in (44, 24) and d != 72:
         continue
-    if (91 <= var < 100 and name != "siglip224") or (var == 8 and name != "gemma224"):
+    if (var == 7 and name != "siglip224") or (var == 8 and name != "gemma224"):
         continue
     NN.check(eng.lib.pgmi_tune_attention(var))
     scale = d ** -0.5

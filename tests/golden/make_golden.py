@@ -20,6 +20,8 @@ What is captured:
   small_ablation_bf16.npz  the same on the 2+2-layer model, every logit kept (the oracle's check)
   full_ablation_bf16.npz  the ablation harness itself (run_inference with load_model_simple's two
                     patches): KV mode 64 tokens incl. the step-0 prompt re-feed, no-KV mode 48 tokens
+  full_batch8_bf16.npz  configs[3]: 8 distinct images, each run alone through inference.test_inference
+  full_batch8_fp32.npz  the fp32 truth of each of those 8 rows, teacher-forced on its bf16 token path
 """
 from __future__ import annotations
 
@@ -371,6 +373,37 @@ def make_batch_images(n_tokens=64, n_sample=256):
     print("full_batch8_bf16.npz written")
 
 
+def make_batch_fp32():
+    """fp32 truth for every row of full_batch8_bf16.npz: the reference model in fp32, teacher-forced on
+    that image's bf16 reference tokens (the path its inference.test_inference run took), the same
+    sampled logit columns per step -- so each batched row gets SURVEY.md sec.8c's "<= 1.5x the
+    reference-bf16 error vs fp32" rule, not image 0 alone."""
+    G = np.load(os.path.join(HERE, "full_batch8_bf16.npz"))
+    cfg = W.full_config(224)
+    sidx = G["sample_idx"]
+    model, _ = build_model(cfg, torch.float32)
+    out_vals = []
+    for i in range(G["ids"].shape[0]):
+        ids = G["ids"][i][None]
+        toks = G["tokens"][i].reshape(-1)
+        px = torch.from_numpy(pixels_from_u8(G["u8"][i])[None])
+        kv = RG.KVCache()
+        mask = torch.ones((1, ids.shape[1]), dtype=torch.int64)
+        cur = torch.from_numpy(ids)
+        fl = []
+        t0 = time.time()
+        with torch.no_grad():
+            for step in range(toks.shape[0]):
+                out = model(input_ids=cur, pixel_values=px if step == 0 else None, attention_mask=mask, kv_cache=kv)
+                fl.append(out["logits"][:, -1, :].float().numpy()[:, sidx])
+                cur = torch.tensor([[int(toks[step])]])
+                mask = torch.cat([mask, torch.ones((1, 1))], dim=-1)
+        out_vals.append(np.concatenate(fl, 0))
+        print(f"image {i}: fp32 teacher-forced {toks.shape[0]} steps in {time.time() - t0:.1f}s")
+    np.savez_compressed(os.path.join(HERE, "full_batch8_fp32.npz"), sample_idx=sidx, sample_vals=np.stack(out_vals))
+    print("full_batch8_fp32.npz written")
+
+
 def make_long(pixels, n_tokens=256):
     """configs[1] as BASELINE.json states it: 256 greedy tokens with the KV cache (KV length up to
     L + 256 + 1), through inference.test_inference, plus the prefill's ALL-ROW logits
@@ -486,13 +519,16 @@ def make_ablation(n_kv=64, n_nokv=48, small=False):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["batch8", "long", "ablation"], default=None,
+    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation"], default=None,
                     help="generate only one later round's fixtures (full_batch8 / full256 / full_ablation)")
     a = ap.parse_args()
     torch.set_num_threads(8)
-    px = make_pixels() if a.only not in ("batch8", "ablation") else None
+    px = make_pixels() if a.only not in ("batch8", "batch8_fp32", "ablation") else None
     if a.only == "batch8":
         make_batch_images()
+        make_batch_fp32()
+    elif a.only == "batch8_fp32":
+        make_batch_fp32()
     elif a.only == "ablation":
         make_ablation(16, 8, small=True)
         make_ablation()
@@ -503,6 +539,7 @@ if __name__ == "__main__":
         if not a.skip_full:
             make_full(px)
             make_batch_images()
+            make_batch_fp32()
             make_long(px)
             make_ablation(16, 8, small=True)
             make_ablation()

@@ -7,7 +7,9 @@ alone; the reference cannot batch, processing_paligemma.py:80 / modeling_gemma.p
 Rules per row (as tests/test_gpu_full.py applies them to image 0):
   * teacher-forced on the row's reference tokens: |delta| <= 0.25 at the reference's top-8 of
     every step, argmax equal wherever the reference's top-2 margin exceeds 0.25, sampled-logit
-    rel-L2 < 3e-2 on average over the 64 steps;
+    rel-L2 < 3e-2 on average over the 64 steps, and the row's error vs its fp32 truth
+    (tests/golden/full_batch8_fp32.npz: the reference in fp32, teacher-forced on that row's token
+    path) <= 1.5x the reference bf16's own error vs that truth;
   * free-running batched greedy: a row's first divergence sits on a step where its reference is
     indecisive (margin < 0.25).
 """
@@ -36,6 +38,11 @@ def G(golden_dir):
 
 
 @pytest.fixture(scope="module")
+def F(golden_dir):
+    return np.load(os.path.join(golden_dir, "full_batch8_fp32.npz"))
+
+
+@pytest.fixture(scope="module")
 def eng():
     from pgmi import Engine
     e = Engine(W.full_config(224), max_batch=8, max_seq=288, max_kv=384)
@@ -54,7 +61,7 @@ def _inputs(G, B):
 
 @pytest.mark.parametrize("B", [3, 5, 8])
 @torch.no_grad()
-def test_batch_rows_teacher_forced_vs_own_reference(eng, G, B):
+def test_batch_rows_teacher_forced_vs_own_reference(eng, G, F, B):
     ids, px = _inputs(G, B)
     L = ids.shape[1]
     kv = eng.new_kv(B, 384)
@@ -78,6 +85,9 @@ def test_batch_rows_teacher_forced_vs_own_reference(eng, G, B):
         s = ours[b][:, sidx].cpu().numpy()
         err = np.mean([rel(s[t], G["sample_vals"][b, t]) for t in range(N_STEPS)])
         assert err < 3e-2, (b, err)
+        err_ours = np.mean([rel(s[t], F["sample_vals"][b, t]) for t in range(N_STEPS)])
+        err_ref = np.mean([rel(G["sample_vals"][b, t], F["sample_vals"][b, t]) for t in range(N_STEPS)])
+        assert err_ours <= 1.5 * err_ref, (b, err_ours, err_ref)
 
 
 @pytest.mark.parametrize("B", [3, 8])

@@ -1194,8 +1194,10 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         //   Gemma 448 (1056 x 8):              16-row 159.5 | RG4xKSPL2 61.3 | RG2xKSPL2 122.7
         // round 3 (same probe, graph-replayed): the one-pass key-split kernel k_attn_fs (variant 9)
         //   Gemma 224 12.2 (full_pre 15.1) | Gemma 448 31.7 (tiled RG4xKSPL2 52.5) | SigLIP 448 24.4 (31.8);
-        //   SigLIP 224 stays on k_attn_short (6.7 against 10.6)
-        v = head_dim == 256 ? 9 : a.Lk <= 256 ? 7 : 9;
+        //   SigLIP 224 stays on k_attn_short at one image (6.7 against 10.6); at 8 images
+        //   (tools/probes/plan_sweep.py --batch 8, whole tower) k_attn_fs: tower 4204 -> 3835 us
+        const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
+        v = head_dim == 256 ? 9 : (a.Lk <= 256 && rows <= 4096) ? 7 : 9;
     }
     if (v == 9 || v == 91 || v == 92 || v == 94) {  // one pass, keys split over workgroups (auto / 1 / 2 / 4 ranges)
         const int want = v == 9 ? 0 : v - 90;

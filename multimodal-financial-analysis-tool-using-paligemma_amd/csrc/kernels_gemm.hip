@@ -1158,7 +1158,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {2048, 4304, 1152, false, W352w, 1},    // vision fc1            48.6 us (was 91.5)
         {2048, 1152, 4304, false, W288w, 2},    // vision fc2            47.3 us (was 72.2)
         {2048, 2048, 1152, false, W128x128, 1}, // projector             19.1 us (was 23.8)
-        {2304, 2560, 2048, false, W288w, 1},    // text q|k|v            32.8 us (was 48.3)
+        {2304, 2560, 2048, false, Q256w, 1},    // text q|k|v            in situ LM 9047 -> 8902 us vs W288w + RoPE
+                                                // epilogue (61 us in situ: 160 workgroups); RoPE by k_rope_kv
         {2304, 2048, 2048, false, W288n, 1},    // text o_proj           35.4 us (was 62.1)
         {2304, 16384, 2048, true, E256, 1},     // text gate|up         261.8 us (W288w 301.8); in situ LM 10064 -> 9435 us
         {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)

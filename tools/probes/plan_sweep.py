@@ -109,7 +109,7 @@ def main():
     for name in (a.shapes or "qkv,out,fc1,fc2,attn").split(","):
         if name == "attn":
             rows = []
-            for v in [41, 42, 21, 22, 44, 24]:
+            for v in [7, 9, 91, 92, 94, 42, 44, 24]:
                 N.check(eng.lib.pgmi_tune_attention(v))
                 rows.append((time_tower(eng, px, a.iters), v))
             N.check(eng.lib.pgmi_tune_attention(-1))

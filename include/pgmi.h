@@ -235,6 +235,14 @@ int pgmi_op_rmsnorm(pgmi_ctx* ctx, const void* x, const void* w, int rows, int D
                     void* stream);
 int pgmi_op_layernorm(pgmi_ctx* ctx, const void* x, const void* w, const void* b, int rows, int D, float eps,
                       void* out, void* stream);
+/* out = bf16(a + b) elementwise over n bf16 values (n a multiple of 8): the residual adds of the per-layer
+ * module forwards (SiglipEncoderLayer.forward modeling_siglip.py:189,202; GemmaDecoderLayer :327,336) */
+int pgmi_op_add(pgmi_ctx* ctx, const void* a, const void* b, int64_t n, void* out, void* stream);
+/* SiglipVisionEmbeddings.forward (modeling_siglip.py:62-79) on given parameters: pixels (B, C, H, H)
+ * bf16 or fp32 (pixel_dtype), conv weight [D][C][P][P] + bias [D], position embedding [(H/P)^2][D]
+ * -> out (B, (H/P)^2, D) bf16 = bf16(bf16(conv + bias) + pos); uses the context's scratch */
+int pgmi_op_patch_embed(pgmi_ctx* ctx, const void* pixels, int pixel_dtype, int B, int C, int H, int P,
+                        const void* conv_w, const void* conv_b, const void* pos, int D, void* out, void* stream);
 /* attention over q (B, Lq, H, hd), k/v (B, Lk, Hkv, hd) -> o (B, Lq, H, hd), all contiguous bf16;
  * s = bf16(bf16(q.k) * scale) */
 int pgmi_op_attention(pgmi_ctx* ctx, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk,

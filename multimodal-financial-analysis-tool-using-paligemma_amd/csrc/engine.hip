@@ -1279,6 +1279,45 @@ int pgmi_op_layernorm(pgmi_ctx* x, const void* in, const void* w, const void* b,
     return 0;
 }
 
+int pgmi_op_add(pgmi_ctx* x, const void* a, const void* b, int64_t n, void* out, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (!a || !b || !out || n < 0) return fail(PGMI_E_ARG, "bad argument");
+    if (n % 8 != 0) return fail(PGMI_E_ARG, "n must be a multiple of 8");
+    if (n == 0) return 0;
+    add_rows((hipStream_t)stream, reinterpret_cast<const uint16_t*>(a), reinterpret_cast<const uint16_t*>(b), (long)n,
+             reinterpret_cast<uint16_t*>(out));
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_patch_embed(pgmi_ctx* x, const void* pixels, int pixel_dtype, int B, int C, int H, int P, const void* conv_w,
+                        const void* conv_b, const void* pos, int D, void* out, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (!pixels || !conv_w || !conv_b || !pos || !out) return fail(PGMI_E_ARG, "null argument");
+    if (pixel_dtype != PGMI_DTYPE_F32 && pixel_dtype != PGMI_DTYPE_BF16) return fail(PGMI_E_ARG, "pixels must be fp32 or bf16");
+    if (B < 1 || C < 1 || P < 1 || H < P || H % P != 0 || D < 1 || D % 8 != 0) return fail(PGMI_E_ARG, "bad shape");
+    const int N = (H / P) * (H / P), K = C * P * P, Kpad = (K + 63) / 64 * 64;
+    // scratch: the conv weight padded to Kpad columns, then the patch rows (modeling_siglip.py:67 as a GEMM)
+    const size_t wbytes = ((size_t)D * Kpad * 2 + 255) & ~(size_t)255, pbytes = ((size_t)B * N * Kpad * 2 + 255) & ~(size_t)255;
+    if (wbytes + pbytes > x->ws_bytes) return fail(PGMI_E_ARG, "batch too large for the scratch");
+    hipStream_t s = (hipStream_t)stream;
+    uint16_t* wpad = reinterpret_cast<uint16_t*>(x->ws);
+    uint16_t* rows = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(x->ws) + wbytes);
+    pad_rows(s, reinterpret_cast<const uint16_t*>(conv_w), D, K, Kpad, wpad);
+    patchify(s, pixels, pixel_dtype == PGMI_DTYPE_F32, B, C, H, H, P, Kpad, rows);
+    EpiArgs e{};
+    e.bias = reinterpret_cast<const uint16_t*>(conv_b);
+    e.pos = reinterpret_cast<const uint16_t*>(pos);
+    e.npos = N;
+    e.out = reinterpret_cast<uint16_t*>(out);
+    e.ldo = D;
+    float* gws = reinterpret_cast<float*>(reinterpret_cast<char*>(x->ws) + wbytes + pbytes);
+    gemm(s, rows, Kpad, wpad, Kpad, B * N, D, Kpad, EPI_BIAS_POS, e, gws, x->ws_bytes - wbytes - pbytes);
+    LAUNCHCHK();
+    return 0;
+}
+
 int pgmi_op_attention(pgmi_ctx* x, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk, int H,
                       int Hkv, int hd, float scale, void* stream) {
     if (!x) return fail(PGMI_E_ARG, "null ctx");

@@ -220,6 +220,25 @@ __global__ void k_scale(const uint16_t* __restrict__ x, long n, float a, uint16_
     }
 }
 
+__global__ void k_add(const uint16_t* __restrict__ x, const uint16_t* __restrict__ y, long n, uint16_t* __restrict__ out) {
+    for (long i = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 8; i < n; i += (long)gridDim.x * blockDim.x * 8) {
+        const uint4 u = ldg16(x + i), v = ldg16(y + i);
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&u);
+        const uint16_t* f = reinterpret_cast<const uint16_t*>(&v);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = f2bf(bf2f(e[j]) + bf2f(f[j]));
+        *reinterpret_cast<u16x8*>(out + i) = o;
+    }
+}
+
+void add_rows(hipStream_t s, const uint16_t* x, const uint16_t* y, long n, uint16_t* out) {
+    long blocks = (n / 8 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_add, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n, out);
+}
+
 void scale_rows(hipStream_t s, const uint16_t* x, long n, float a, uint16_t* out) {
     long blocks = (n / 8 + 255) / 256;
     if (blocks > 4096) blocks = 4096;

@@ -147,6 +147,7 @@ void merge_embed(hipStream_t s, const int64_t* ids, int B, int L, const uint16_t
                  const uint16_t* img, int n_img_rows, int64_t image_token, int64_t pad_id, float sqrt_h,
                  float normalizer, const uint16_t* embeds_in, int* scan_buf, uint16_t* out);
 void scale_rows(hipStream_t s, const uint16_t* x, long n, float normalizer, uint16_t* out);
+void add_rows(hipStream_t s, const uint16_t* x, const uint16_t* y, long n, uint16_t* out);  // bf16(x + y), n % 8 == 0
 // qkv: bf16 [B*L][(nh+2nkv)*256], or (split > 1) the fp32 partial slabs ws[split][B*L][...]
 void rope_kv_append(hipStream_t s, const uint16_t* qkv, const float* ws, int split, int B, int L, int nh, int nkv,
                     const int64_t* pos, const uint16_t* cosT, const uint16_t* sinT, int max_pos, uint16_t* q_out,

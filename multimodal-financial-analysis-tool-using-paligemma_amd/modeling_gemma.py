@@ -29,6 +29,7 @@ from torch.nn import CrossEntropyLoss
 
 from modeling_siglip import SiglipVisionConfig, SiglipVisionModel
 from pgmi import binding as _binding
+from pgmi import modules as _modules
 from pgmi.lazy_logits import LazyLogits
 
 
@@ -151,7 +152,7 @@ class GemmaRMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.zeros(dim))
 
-    forward = _fused("GemmaRMSNorm")
+    forward = _modules.gemma_rmsnorm_forward  # callable on its own (pgmi_op_rmsnorm)
 
 
 class GemmaMLP(nn.Module):
@@ -166,7 +167,7 @@ class GemmaMLP(nn.Module):
         self.up_proj = nn.Linear(self.hidden_size, self.intermediate_size, bias=False)
         self.down_proj = nn.Linear(self.intermediate_size, self.hidden_size, bias=False)
 
-    forward = _fused("GemmaMLP")
+    forward = _modules.gemma_mlp_forward  # callable on its own (pgmi_op_gemm: GeGLU, then down)
 
 
 def repeat_kv(hidden_states: torch.Tensor, n_rep: int) -> torch.Tensor:

@@ -4,8 +4,9 @@ The module tree, constructor signatures and state-dict names are the reference's
 (/root/reference/modeling_siglip.py:7-255), so checkpoints load unchanged.  The forward of
 SiglipVisionModel runs the whole tower in libpgmi (pgmi_vision: im2col+MFMA patch embedding,
 27 x [LayerNorm, fused QKV GEMM, MHA, out-proj+residual, LayerNorm, fc1+GELU, fc2+residual],
-post-LayerNorm; csrc/engine.hip).  The per-layer submodules keep their parameters but their
-own forward() is not a separate entry point: the layers are fused into that one call.
+post-LayerNorm; csrc/engine.hip).  The per-layer submodules (embeddings, attention, MLP, encoder
+layer, encoder) are callable on their own too, on libpgmi's single-op entries (pgmi/modules.py), so
+forward hooks on them fire when they are called; the fused tower does not call them.
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from pgmi import binding as _binding
+from pgmi import modules as _modules
 
 
 class SiglipVisionConfig:
@@ -36,12 +38,11 @@ class SiglipVisionConfig:
         self.num_image_tokens = num_image_tokens
 
 
-def _fused(name):
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError(
-            f"{name}.forward is fused into libpgmi's vision tower; call SiglipVisionModel (or the PaliGemma "
-            "model) instead")
-    return forward
+class _LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters and state-dict names) whose own forward runs pgmi_op_layernorm."""
+
+    def forward(self, x):
+        return _modules.layer_norm(x, self.weight, self.bias, self.eps)
 
 
 class SiglipVisionEmbeddings(nn.Module):
@@ -60,7 +61,7 @@ class SiglipVisionEmbeddings(nn.Module):
         self.position_embedding = nn.Embedding(self.num_positions, self.embed_dim)
         self.register_buffer("position_ids", torch.arange(self.num_positions).expand((1, -1)), persistent=False)
 
-    forward = _fused("SiglipVisionEmbeddings")
+    forward = _modules.siglip_embeddings_forward
 
 
 class SiglipAttention(nn.Module):
@@ -79,7 +80,7 @@ class SiglipAttention(nn.Module):
         self.q_proj = nn.Linear(self.embed_dim, self.embed_dim)
         self.out_proj = nn.Linear(self.embed_dim, self.embed_dim)
 
-    forward = _fused("SiglipAttention")
+    forward = _modules.siglip_attention_forward
 
 
 class SiglipMLP(nn.Module):
@@ -91,7 +92,7 @@ class SiglipMLP(nn.Module):
         self.fc1 = nn.Linear(config.hidden_size, config.intermediate_size)
         self.fc2 = nn.Linear(config.intermediate_size, config.hidden_size)
 
-    forward = _fused("SiglipMLP")
+    forward = _modules.siglip_mlp_forward
 
 
 class SiglipEncoderLayer(nn.Module):
@@ -101,11 +102,11 @@ class SiglipEncoderLayer(nn.Module):
         super().__init__()
         self.embed_dim = config.hidden_size
         self.self_attn = SiglipAttention(config)
-        self.layer_norm1 = nn.LayerNorm(self.embed_dim, eps=config.layer_norm_eps)
+        self.layer_norm1 = _LayerNorm(self.embed_dim, eps=config.layer_norm_eps)
         self.mlp = SiglipMLP(config)
-        self.layer_norm2 = nn.LayerNorm(self.embed_dim, eps=config.layer_norm_eps)
+        self.layer_norm2 = _LayerNorm(self.embed_dim, eps=config.layer_norm_eps)
 
-    forward = _fused("SiglipEncoderLayer")
+    forward = _modules.siglip_encoder_layer_forward
 
 
 class SiglipEncoder(nn.Module):
@@ -116,7 +117,7 @@ class SiglipEncoder(nn.Module):
         self.config = config
         self.layers = nn.ModuleList([SiglipEncoderLayer(config) for _ in range(config.num_hidden_layers)])
 
-    forward = _fused("SiglipEncoder")
+    forward = _modules.siglip_encoder_forward
 
 
 class SiglipVisionTransformer(nn.Module):
@@ -127,7 +128,7 @@ class SiglipVisionTransformer(nn.Module):
         self.config = config
         self.embeddings = SiglipVisionEmbeddings(config)
         self.encoder = SiglipEncoder(config)
-        self.post_layernorm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.post_layernorm = _LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
 
     def forward(self, pixel_values: torch.Tensor) -> torch.Tensor:
         return _binding.vision_forward(self, pixel_values, prefix="vision_tower.vision_model.")

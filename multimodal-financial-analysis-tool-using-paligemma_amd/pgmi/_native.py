@@ -86,6 +86,8 @@ SIGNATURES = {
     "pgmi_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, f32, vp, vp]),
     "pgmi_op_layernorm": (i32, [vp, vp, vp, vp, i32, i32, f32, vp, vp]),
     "pgmi_op_attention": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp]),
+    "pgmi_op_add": (i32, [vp, vp, vp, i64, vp, vp]),
+    "pgmi_op_patch_embed": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
     "pgmi_op_gemv_res": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
 }
 

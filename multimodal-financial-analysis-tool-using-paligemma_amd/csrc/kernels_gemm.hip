@@ -1151,7 +1151,7 @@ static Plan choose(int M, int N, int K, bool dual) {
         {1024, 3456, 1152, false, W128x128, 1}, // 448 px vision q|k|v   18.3 us (was 24.6)
         {1024, 1152, 1152, false, P96x64s4, 1}, // 448 px vision out     10.6 us (P32x64s4 13.7)
         {1024, 4304, 1152, false, W288w, 1},    // 448 px vision fc1     25.1 us (exp/rcp GELU; was 29.5)
-        {1024, 1152, 4304, false, W288w, 4},    // 448 px vision fc2     31.7 us (W128x128 split 2: 35.9)
+        {1024, 1152, 4304, false, W128x128, 3}, // 448 px vision fc2     in situ tower 2965 -> 2904 us vs W288w split 4
         // configs[3]: 8 images per GPU as one batch (vision 2048 rows, text 2304 rows), cold sweep
         {2048, 3456, 1152, false, W288w, 1},    // vision q|k|v          31.2 us (was 46.8)
         {2048, 1152, 1152, false, W128x128, 1}, // vision out_proj       22.3 us (was 31.6)

@@ -85,6 +85,15 @@ def main():
         ref = ref.clone()
         print(f"lm forward (current plans): {base:.1f} us", flush=True)
         for name in (a.shapes or "qkv,o,gateup,down").split(","):
+            if name == "attn":
+                rows = []
+                for v in [9, 91, 92, 94, 8, 42]:
+                    N.check(eng.lib.pgmi_tune_attention(v))
+                    rows.append((time_lm(eng, args, a.iters)[0], v))
+                N.check(eng.lib.pgmi_tune_attention(-1))
+                rows.sort()
+                print("attn: " + ", ".join(f"v{v}: {t:.1f}" for t, v in rows), flush=True)
+                continue
             Mm, Nn, K, dual, splits = shapes[name]
             if a.splits and not dual:
                 splits = [int(x) for x in a.splits.split(",")]

@@ -34,6 +34,6 @@ python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_trace.csv $OUT/mfma/run_cou
 python3 $R/tools/kernel_pmc.py $OUT/ptrace/run_kernel_trace.csv - \
     $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_hbm_probe.csv >> $OUT/summary.txt
 echo done
-python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
+PGMI_ROUND=$TAG python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     "k_gemv<1, 4, 1, 2, 1, true, 1, false>" gateup $OUT/pmc_traffic.json >> $OUT/summary.txt
 echo traffic done

@@ -24,26 +24,28 @@ namespace pgmi {
 constexpr int MF_MAXB = 16;
 
 // RMSNorm'd (or plain) activation rows into xs (stride ld).  Every row's chunks are loaded
-// before any is reduced (one round trip for the whole [nb][K] block, not one per row).
-__device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red, int k0 = 0, int ksl = -1) {
-    if (ksl < 0) ksl = K;  // stage columns [k0, k0 + ksl) at xs column 0; the norm uses the whole row
+// before any is reduced (one round trip for the whole [nb][K] block, not one per row).  NBM: rows
+// loaded per chunk (unconditionally, rows past nb clamped to the last one); 8 when nb <= 8, so
+// batches up to 8 issue half the loads of the 16-row form (mf_stage_rows picks it per launch).
+template <int NBM>
+__device__ void mf_stage_rows_t(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red, int k0, int ksl) {
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-    float ss[MF_MAXB];
+    float ss[NBM];
 #pragma unroll
-    for (int b = 0; b < MF_MAXB; ++b) ss[b] = 0.f;
+    for (int b = 0; b < NBM; ++b) ss[b] = 0.f;
     // K <= 8 x threads (K = 2048 at 256 or 512 threads): one chunk per thread, and its norm weights are
     // fetched with the rows (one round trip, not a second one after the reduction)
     const bool one = (K <= nt * 8);
     const bool has = tid * 8 < K;
     const uint4 wv0 = (one && a.norm_w) ? ldg16(a.norm_w + (has ? tid * 8 : 0)) : make_uint4(0, 0, 0, 0);
     for (int c = tid * 8; c < K; c += nt * 8) {
-        uint4 v[MF_MAXB];
+        uint4 v[NBM];
 #pragma unroll
-        for (int b = 0; b < MF_MAXB; ++b)  // unconditional (clamped row): the loads stay in flight together
+        for (int b = 0; b < NBM; ++b)  // unconditional (clamped row): the loads stay in flight together
             v[b] = ldg16(a.x + (long)(b < a.nb ? b : a.nb - 1) * K + c);
         const bool mine = c >= k0 && c < k0 + ksl;
 #pragma unroll
-        for (int b = 0; b < MF_MAXB; ++b)
+        for (int b = 0; b < NBM; ++b)
             if (b < a.nb) {
                 if (mine) *reinterpret_cast<uint4*>(xs + b * ld + (c - k0)) = v[b];
                 const uint16_t* e = reinterpret_cast<const uint16_t*>(&v[b]);
@@ -53,15 +55,15 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
     }
     if (!a.norm_w) return;
 #pragma unroll
-    for (int b = 0; b < MF_MAXB; ++b)
+    for (int b = 0; b < NBM; ++b)
         if (b < a.nb) {
             const float t = wave_sum(ss[b]);
             if (lane == 0) red[b * 16 + wave] = t;
         }
     __syncthreads();
-    float r[MF_MAXB];
+    float r[NBM];
 #pragma unroll
-    for (int b = 0; b < MF_MAXB; ++b) {
+    for (int b = 0; b < NBM; ++b) {
         float t = 0.f;
         if (b < a.nb)
             for (int w = 0; w < nw; ++w) t += red[b * 16 + w];  // fixed order
@@ -72,7 +74,7 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
         const uint4 wv = one ? wv0 : ldg16(a.norm_w + c);
         const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
 #pragma unroll
-        for (int b = 0; b < MF_MAXB; ++b)
+        for (int b = 0; b < NBM; ++b)
             if (b < a.nb) {
                 const uint4 v = *reinterpret_cast<const uint4*>(xs + b * ld + (c - k0));
                 const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
@@ -84,10 +86,20 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
     }
 }
 
+__device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, float* red, int k0 = 0, int ksl = -1) {
+    if (ksl < 0) ksl = K;  // stage columns [k0, k0 + ksl) at xs column 0; the norm uses the whole row
+    if (a.nb <= 8) mf_stage_rows_t<8>(a, K, xs, ld, red, k0, ksl);  // uniform branch: each form drains its own loads
+    else mf_stage_rows_t<MF_MAXB>(a, K, xs, ld, red, k0, ksl);
+}
+
 // MODE: GV_*; NR: weight rows per unit (2: RoPE / GeGLU pairs); KW: K elements per wave; WK:
 // waves per unit group (K split inside the workgroup).  grid.x: unit-group slots (grid-stride
 // over groups), grid.y: KS (K split over workgroups; GV_RES only, partials to ws).
-template <int MODE, int NR, int KW, int WK>
+// PF = 2 (GV_RES, no staging): the streams of a workgroup's next TWO groups are in flight while a
+// group multiplies -- two register buffers in ping-pong, every issue unconditional (groups past the
+// end read one 64-B line of the matrix: all lanes the same address, results discarded), so the
+// compiler's in-order vmcnt keeps the second stream in flight across the first's wait.
+template <int MODE, int NR, int KW, int WK, int PF = 1>
 __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restrict__ ws) {
     constexpr int NKB = KW / 128;          // 128-wide k blocks per wave
     constexpr bool STAGE = (MODE != GV_RES);
@@ -127,6 +139,65 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 for (int i = 0; i < 4; ++i) w[j][kb][i] = ldg_nt(rp + kb * 128 + 32 * i);
         }
     };
+    if constexpr (PF == 2) {
+        static_assert(MODE == GV_RES && NR == 1, "two-deep stream: K-split residual projection only");
+        uint4 wb[2][NKB][4];
+        auto issue_into = [&](uint4 (&dst)[NKB][4], int gi) {
+            const bool live = gi < n_groups;
+            const uint16_t* rp = live ? a.W + (long)(gi * 16 + n < a.n_units ? gi * 16 + n : a.n_units - 1) * K + k0 + 8 * g
+                                      : a.W;
+            const int step = live ? 1 : 0;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dst[kb][i] = ldg_nt(rp + step * (kb * 128 + 32 * i));
+        };
+        const int G = gridDim.x;
+        // activation rows n >= nb re-read row nb - 1 (unconditional loads): they only feed C rows
+        // b >= nb, which are never stored
+        short8 xr[NKB][4];
+        const int xrow = n < a.nb ? n : a.nb - 1;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xr[kb][i] = __builtin_bit_cast(short8, ldg16(a.x + (long)xrow * K + k0 + kb * 128 + 32 * i + 8 * g));
+        // the activation before the two streams: the first multiply waits for xr and the first
+        // stream only (in-order vmcnt), the second stream stays in flight
+        issue_into(wb[0], blockIdx.x);
+        issue_into(wb[1], blockIdx.x + G);
+        auto step = [&](uint4 (&buf)[NKB][4], int cur) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = mfma16(xr[kb][i], __builtin_bit_cast(short8, buf[kb][i]), acc);
+            issue_into(buf, cur + 2 * G);  // this buffer's next stream starts now
+            if constexpr (WK > 1) {
+                kred[wk][0][lane] = acc;
+                __syncthreads();
+                if (wk == 0)
+#pragma unroll
+                    for (int q = 1; q < WK; ++q) acc += kred[q][0][lane];
+                __syncthreads();
+            }
+            const int u = cur * 16 + n;
+            if (wk == 0 && cur < n_groups && u < a.n_units)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int b = 4 * g + r;
+                    if (b >= a.nb) break;
+                    ws[((long)ks * a.nb + b) * a.n_units + u] = acc[r];  // K split only (no load in the loop)
+                }
+        };
+        // pairs of groups per trip; the trip count is uniform over the grid, and a group past the
+        // end multiplies the dummy line and stores nothing (no branch around any load)
+        for (int g0 = blockIdx.x; g0 - (int)blockIdx.x < n_groups; g0 += 2 * G) {
+            step(wb[0], g0);
+            step(wb[1], g0 + G);
+        }
+        return;
+    }
     int grp = blockIdx.x;
     if (grp < n_groups) issue(grp);
     // RoPE operands of this workgroup's first group, fetched with the weight stream (the epilogue
@@ -444,9 +515,12 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
 }
 
 // flash-decoding combine of k_attn_decode's partials -> o (bf16 [nb][G*256]), one thread per
-// 8 outputs, chunk records in a fixed order (gemv_body.h's GV_ORES prologue, once per output)
-__global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __restrict__ o, int K) {
-    const int e8 = blockIdx.x * 256 + threadIdx.x;
+// 8 outputs, chunk records in a fixed order (gemv_body.h's GV_ORES prologue, once per output).
+// As that prologue: up to CMAX chunk records are loaded unconditionally up front (chunk index
+// clamped, records past nch ignored), so the combine costs one memory round trip instead of one
+// per chunk; 64-thread workgroups spread the 2,048 threads of B = 8 over 32 CUs.
+__global__ void __launch_bounds__(64) k_attn_combine(GemvArgs a, uint16_t* __restrict__ o, int K) {
+    const int e8 = blockIdx.x * 64 + threadIdx.x;
     if (e8 >= a.nb * K / 8) return;
     const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
     const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
@@ -456,14 +530,39 @@ __global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __re
     float M = -INFINITY, S = 0.f, acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
-    for (int c = 0; c < nch; ++c) {
-        const float wgt = expf(sp[(long)c * kAttnPartStride] - M);
-        S += wgt * sp[(long)c * kAttnPartStride + 16];
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+    constexpr int CMAX = 12;  // chunks held in registers (768 keys); longer caches take the loop
+    if (nch <= CMAX) {
+        f32x4 x0[CMAX], x1[CMAX];
+        float mc[CMAX], lc[CMAX];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { acc[j] += wgt * x0[j]; acc[4 + j] += wgt * x1[j]; }
+        for (int c = 0; c < CMAX; ++c) {
+            const long cs = (long)(c < nch ? c : nch - 1) * kAttnPartStride;
+            x0[c] = *reinterpret_cast<const f32x4*>(pb + cs);
+            x1[c] = *reinterpret_cast<const f32x4*>(pb + cs + 4);
+            mc[c] = sp[cs];
+            lc[c] = sp[cs + 16];
+        }
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < nch) M = fmaxf(M, mc[c]);
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < nch) {
+                const float wgt = expf(mc[c] - M);
+                S += wgt * lc[c];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { acc[j] += wgt * x0[c][j]; acc[4 + j] += wgt * x1[c][j]; }
+            }
+    } else {
+        for (int c = 0; c < nch; ++c) M = fmaxf(M, sp[(long)c * kAttnPartStride]);
+        for (int c = 0; c < nch; ++c) {
+            const float wgt = expf(sp[(long)c * kAttnPartStride] - M);
+            S += wgt * sp[(long)c * kAttnPartStride + 16];
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(pb + (long)c * kAttnPartStride + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { acc[j] += wgt * x0[j]; acc[4 + j] += wgt * x1[j]; }
+        }
     }
     u16x8 ob;
 #pragma unroll
@@ -472,27 +571,41 @@ __global__ void __launch_bounds__(256) k_attn_combine(GemvArgs a, uint16_t* __re
 }
 
 // h[b][n] = bf16(bf16(sum_ks ws[ks][b][n]) + h[b][n]), fixed ks order
+// (KS <= 8: the eight slab loads and the residual load are issued unconditionally up front -- slab
+// index clamped, slabs past KS left out of the sum by a select after the loads -- so the combine is
+// one memory round trip, not one per slab; the sum keeps the slab order)
 __global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N, uint16_t* __restrict__ h) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nb * N) return;
-    float s = ws[i];
-    for (int q = 1; q < KS; ++q) s += ws[(long)q * nb * N + i];
+    const long slab = (long)nb * N;
+    float s;
+    if (KS <= 8) {
+        float p[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p[q] = ws[(long)(q < KS ? q : 0) * slab + i];
+        s = p[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) s = q < KS ? s + p[q] : s;
+    } else {
+        s = ws[i];
+        for (int q = 1; q < KS; ++q) s += ws[(long)q * slab + i];
+    }
     h[i] = f2bf(rbf(s) + bf2f(h[i]));
 }
 
 // smallest lock-step batch whose decode projections run on MFMA (B <= 2: the v_dot2 GEMVs of gemv_body.h)
 int gemv_mf_min_batch() { return 3; }
 
-template <int MODE, int NR, int KW, int WK>
+template <int MODE, int NR, int KW, int WK, int PF = 1>
 static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
     const size_t lds = (MODE == GV_RES) ? 0 : (size_t)a.nb * (a.K + 8) * sizeof(uint16_t);
     static size_t attr = 0;
     if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK, PF>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
+    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK, PF>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
 }
 
 static int groups_of(int units) { return (units + 15) / 16; }
@@ -537,7 +650,7 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     const int K = a.K;
-    hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 255) / 256), dim3(256), 0, s, a, o, K);
+    hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 63) / 64), dim3(64), 0, s, a, o, K);
     GemvArgs r = a;
     r.x = o;
     r.norm_w = nullptr;
@@ -565,7 +678,7 @@ void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws) {
         // register-streamed MFMA form, 4 waves x 512 of each 2,048-wide K slice, 32 x 8 workgroups
         // (every row group of a slice once): B = 8 step 1.737 -> 1.704 ms against the LDS-DMA ring
         // (64 / 128 x 8 workgroups: 1.710 / 1.744)
-        launch_mf<GV_RES, 1, 512, 4>(s, a, 32, KS, ws);
+        launch_mf<GV_RES, 1, 512, 4, 2>(s, a, 32, KS, ws);
         const int nn = a.nb * a.n_units;
         hipLaunchKernelGGL(k_mf_combine, dim3((nn + 255) / 256), dim3(256), 0, s, ws, KS, a.nb, a.n_units, a.out);
         return;

@@ -164,29 +164,42 @@ def time_preprocess(eng, dev, size, iters=20):
     return round(e0.elapsed_time(e1) / iters, 4)
 
 
-def gemm_roofline(eng, rows, iters=36):
+def gemm_roofline(eng, rows, iters=36, reps=4):
     """The prefill's dominant MFMA GEMMs (gate|up + GeGLU, down) of all 18 layers over `rows`
-    token rows, timed with HIP events on the stream they are launched on."""
+    token rows.  `iters` launches cycling the layers (cold weights: 18 layers x 134 / 67 MB stream
+    past the 256 MiB MALL) are captured into one graph and replayed `reps` times back to back;
+    HIP events on the replay stream give the average launch, graph gaps included (an eager
+    ctypes loop is host-bound for a ~20 us kernel: round 3 read 38 us for a 23 us kernel)."""
     import torch
     from pgmi import _native as N
     t = eng.cfgd
     H, I, nl = t["t_hidden"], t["t_intermediate"], t["t_layers"]
-    s = torch.cuda.current_stream()
     out = {}
     for which, name, flops in ((0, "gate_up_geglu", 2.0 * rows * 2 * I * H), (1, "down", 2.0 * rows * H * I)):
-        for i in range(nl):
-            N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i, rows, s.cuda_stream))
+        cur = torch.cuda.current_stream()
+        for i in range(nl):  # eager warm-up (kernel attributes are set on first use, outside the capture)
+            N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i, rows, cur.cuda_stream))
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cs = torch.cuda.current_stream()
+            for i in range(iters):
+                N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i % nl, rows, cs.cuda_stream))
+        g.replay()
+        torch.cuda.synchronize()
         k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        k0.record(s)
-        for i in range(iters):
-            N.check(eng.lib.pgmi_prefill_kernel(eng.ctx, which, i % nl, rows, s.cuda_stream))
-        k1.record(s)
+        k0.record()
+        for _ in range(reps):
+            g.replay()
+        k1.record()
         k1.synchronize()
-        us = k0.elapsed_time(k1) * 1e3 / iters
+        us = k0.elapsed_time(k1) * 1e3 / (iters * reps)
+        del g
         tfs = flops / (us * 1e-6) / 1e12
         out[name] = {"bound": "mfma", "rows": rows, "flop_per_launch": int(flops), "avg_launch_us": round(us, 2),
                      "achieved": round(tfs, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(tfs / MFMA_BF16_PEAK_TFS, 4)}
+                     "frac": round(tfs / MFMA_BF16_PEAK_TFS, 4),
+                     "timing": f"{iters} launches cycling the {nl} layers in one graph, replayed {reps}x, HIP events"}
     return out
 
 

@@ -247,6 +247,27 @@ int pgmi_op_patch_embed(pgmi_ctx* ctx, const void* pixels, int pixel_dtype, int 
  * s = bf16(bf16(q.k) * scale) */
 int pgmi_op_attention(pgmi_ctx* ctx, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk,
                       int H, int Hkv, int head_dim, float scale, void* stream);
+/* Reference-order attention of the module forwards (SiglipAttention.forward modeling_siglip.py:116-131,
+ * GemmaAttention.forward modeling_gemma.py:262-277), returning the probability matrix the reference
+ * returns as its second output:
+ *   s = bf16(q.k); s = bf16(s * scale) (scale_div 0) or bf16(s / scale) (scale_div 1, Gemma's
+ *   "/ math.sqrt(head_dim)"); + mask (additive, optional: bf16 -> bf16(s + m), fp32 -> s + m in fp32,
+ *   as torch promotes); p = bf16(softmax_fp32(s)); o = bf16(p.v).  q/o (B, Lq, H, hd); k/v
+ *   (B, Lk, Hkv, hd) for kv_layout 0 or (B, Hkv, Lk, hd) for kv_layout 1 (the KVCache layout);
+ *   query head h reads KV head h / (H / Hkv) (repeat_kv, :136-141).  mask element (b, h, i, j) at
+ *   b*m_b_stride + h*m_h_stride + i*m_q_stride + j (a stride of 0 broadcasts).  probs (B, H, Lq, Lk)
+ *   bf16, may be NULL.  hd <= 256. */
+int pgmi_op_attention_ex(pgmi_ctx* ctx, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk,
+                         int H, int Hkv, int head_dim, int kv_layout, float scale, int scale_div, const void* mask,
+                         int mask_dtype, int64_t m_b_stride, int64_t m_h_stride, int64_t m_q_stride, void* probs,
+                         void* stream);
+/* apply_rotary_pos_emb for one projection (modeling_gemma.py:187-199) with the caller's cos/sin rows
+ * (GemmaRotaryEmbedding.forward's output, :155-185): x (rows, heads*hd) -> out = bf16(bf16(x*cos) +
+ * bf16(rotate_half(x)*sin)), cos/sin bf16 (rows, hd). */
+int pgmi_op_rope(pgmi_ctx* ctx, const void* x, const void* cos_rows, const void* sin_rows, int64_t rows, int heads,
+                 int head_dim, void* out, void* stream);
+/* out = bf16(x * a) over n bf16 values (n a multiple of 8): GemmaModel's normalizer (modeling_gemma.py:367-368) */
+int pgmi_op_scale(pgmi_ctx* ctx, const void* x, float a, int64_t n, void* out, void* stream);
 /* decode GEMV family on one layer's weights (tests): y[b][n] += W x (residual form) */
 int pgmi_op_gemv_res(pgmi_ctx* ctx, const void* x, const void* W, int B, int N, int K, void* h_inout,
                      void* stream);

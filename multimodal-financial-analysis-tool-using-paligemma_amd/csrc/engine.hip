@@ -277,8 +277,8 @@ int ensure_prepared(pgmi_ctx* x) {
 // the library -- need no librccl; the four entry points it uses are resolved once.
 namespace {
 struct Rccl {
-    bool tried = false;
     void* h = nullptr;
+    std::string why;  // dlerror() of the failed load
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
@@ -286,20 +286,24 @@ struct Rccl {
     const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
+// thread-safe one-time load (a function-local static is initialised exactly once)
 Rccl& rccl() {
-    static Rccl r;
-    if (!r.tried) {
-        r.tried = true;
-        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-            if ((r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
-        if (r.h) {
-            r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(r.h, "ncclGetUniqueId"));
-            r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.h, "ncclCommInitRank"));
-            r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.h, "ncclCommDestroy"));
-            r.broadcast = reinterpret_cast<decltype(r.broadcast)>(dlsym(r.h, "ncclBroadcast"));
-            r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.h, "ncclGetErrorString"));
+    static Rccl r = [] {
+        Rccl t;
+        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            if ((t.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+            const char* e = dlerror();
+            if (e) t.why = e;
         }
-    }
+        if (t.h) {
+            t.get_unique_id = reinterpret_cast<decltype(t.get_unique_id)>(dlsym(t.h, "ncclGetUniqueId"));
+            t.comm_init_rank = reinterpret_cast<decltype(t.comm_init_rank)>(dlsym(t.h, "ncclCommInitRank"));
+            t.comm_destroy = reinterpret_cast<decltype(t.comm_destroy)>(dlsym(t.h, "ncclCommDestroy"));
+            t.broadcast = reinterpret_cast<decltype(t.broadcast)>(dlsym(t.h, "ncclBroadcast"));
+            t.error_string = reinterpret_cast<decltype(t.error_string)>(dlsym(t.h, "ncclGetErrorString"));
+        }
+        return t;
+    }();
     return r;
 }
 }  // namespace
@@ -1056,7 +1060,8 @@ int pgmi_lm_final_hidden(pgmi_ctx* x, void* out, int rows, void* stream) {
     do {                                                                                   \
         const Rccl& r_ = rccl();                                                           \
         if (!r_.get_unique_id || !r_.comm_init_rank || !r_.comm_destroy || !r_.broadcast || !r_.error_string) \
-            return fail(PGMI_E_STATE, "librccl could not be loaded (dlopen librccl.so.1)");  \
+            return fail(PGMI_E_STATE, std::string("librccl could not be loaded (dlopen librccl.so.1): ") + \
+                        (r_.h ? "missing nccl* symbols" : r_.why));                        \
     } while (0)
 
 #define NCCLCHK(expr)                                                                      \
@@ -1331,6 +1336,62 @@ int pgmi_op_attention(pgmi_ctx* x, const void* q, const void* k, const void* v, 
     a.Lq = Lq; a.Lk = Lk; a.G = H / Hkv; a.n_kv = Hkv; a.B = B; a.scale = scale;
     a.ws = x->ws; a.ws_floats = (long)(x->ws_bytes / sizeof(float));
     attention_prefill((hipStream_t)stream, hd, a);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_attention_ex(pgmi_ctx* x, const void* q, const void* k, const void* v, void* o, int B, int Lq, int Lk,
+                         int H, int Hkv, int hd, int kv_layout, float scale, int scale_div, const void* mask,
+                         int mask_dtype, int64_t m_b_stride, int64_t m_h_stride, int64_t m_q_stride, void* probs,
+                         void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (!q || !k || !v || !o) return fail(PGMI_E_ARG, "null argument");
+    if (B < 1 || Lq < 1 || Lk < 1 || H < 1 || Hkv < 1 || H % Hkv != 0) return fail(PGMI_E_ARG, "bad shape");
+    if (hd < 1 || hd > 256) return fail(PGMI_E_ARG, "head_dim must be in [1, 256]");
+    if (kv_layout != 0 && kv_layout != 1) return fail(PGMI_E_ARG, "kv_layout must be 0 (B,L,Hkv,hd) or 1 (B,Hkv,L,hd)");
+    if (mask && mask_dtype != PGMI_DTYPE_BF16 && mask_dtype != PGMI_DTYPE_F32)
+        return fail(PGMI_E_ARG, "mask must be bf16 or fp32");
+    if (attention_exact_lds(Lk, hd) > 160 * 1024) return fail(PGMI_E_ARG, "too many keys for one workgroup's scores");
+    ModAttnArgs a{};
+    a.q = reinterpret_cast<const uint16_t*>(q);
+    a.k = reinterpret_cast<const uint16_t*>(k);
+    a.v = reinterpret_cast<const uint16_t*>(v);
+    a.kv_b_stride = (long)Lk * Hkv * hd;
+    a.kv_h_stride = kv_layout == 0 ? hd : (long)Lk * hd;
+    a.kv_row_stride = kv_layout == 0 ? (long)Hkv * hd : hd;
+    a.o = reinterpret_cast<uint16_t*>(o);
+    a.probs = reinterpret_cast<uint16_t*>(probs);
+    a.mask = mask;
+    a.m_b_stride = m_b_stride;
+    a.m_h_stride = m_h_stride;
+    a.m_q_stride = m_q_stride;
+    a.mask_f32 = mask_dtype == PGMI_DTYPE_F32;
+    a.B = B; a.Lq = Lq; a.Lk = Lk; a.H = H; a.Hkv = Hkv; a.hd = hd;
+    a.scale = scale;
+    a.scale_div = scale_div != 0;
+    attention_exact((hipStream_t)stream, a);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_rope(pgmi_ctx* x, const void* in, const void* cos_rows, const void* sin_rows, int64_t rows, int heads,
+                 int hd, void* out, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (!in || !cos_rows || !sin_rows || !out) return fail(PGMI_E_ARG, "null argument");
+    if (rows < 0 || heads < 1 || hd < 2 || hd % 2 != 0) return fail(PGMI_E_ARG, "bad shape");
+    if (rows == 0) return 0;
+    rope_rows((hipStream_t)stream, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(cos_rows),
+              reinterpret_cast<const uint16_t*>(sin_rows), (long)rows, heads, hd, reinterpret_cast<uint16_t*>(out));
+    LAUNCHCHK();
+    return 0;
+}
+
+int pgmi_op_scale(pgmi_ctx* x, const void* in, float a, int64_t n, void* out, void* stream) {
+    if (!x) return fail(PGMI_E_ARG, "null ctx");
+    if (!in || !out || n < 0) return fail(PGMI_E_ARG, "bad argument");
+    if (n % 8 != 0) return fail(PGMI_E_ARG, "n must be a multiple of 8");
+    if (n == 0) return 0;
+    scale_rows((hipStream_t)stream, reinterpret_cast<const uint16_t*>(in), (long)n, a, reinterpret_cast<uint16_t*>(out));
     LAUNCHCHK();
     return 0;
 }

@@ -1414,6 +1414,14 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
     if (p.split > 1 && N % 4 != 0) p.split = 1;  // the split-K epilogue works on 4 outputs per thread
     const long up_off = (long)up_offset_rows * ldw;
     if (defer && p.split > 16) p.split = 16;  // the consumers (splitk_res_norm, rope_kv) reduce at most 16 slabs
+    if (p.split > 1) {
+        // every K range non-empty (a forced split can exceed what K allows: the 8-phase kernel
+        // leaves an empty range's partial slab unwritten, and any empty range is wasted work);
+        // the consumers reduce the split returned here
+        const int nkt = (K + BK - 1) / BK;
+        const int per = (nkt + p.split - 1) / p.split;
+        p.split = (nkt + per - 1) / per;
+    }
     if (defer && p.split > 1) {
         // partial slabs only: the consumer kernel (splitk_res_norm / rope_kv_append) reduces them
         switch (p.cfg) {

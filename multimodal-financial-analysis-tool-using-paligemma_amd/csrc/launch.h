@@ -131,6 +131,28 @@ size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
 void attention_force_variant(int v);  // tuning hook (kernels_attn.hip); -1 = measured choice
 
+// ---------------------------------------------------------------- per-module entry points (kernels_modules.hip)
+// reference-order attention with the probability matrix and an additive mask (module forwards)
+struct ModAttnArgs {
+    const uint16_t* q;           // (B, Lq, H, hd)
+    const uint16_t* k;           // KV head hk of batch b, key j: k + b*kv_b_stride + hk*kv_h_stride + j*kv_row_stride
+    const uint16_t* v;
+    long kv_b_stride, kv_h_stride, kv_row_stride;
+    uint16_t* o;                 // (B, Lq, H, hd)
+    uint16_t* probs;             // (B, H, Lq, Lk) bf16 or nullptr
+    const void* mask;            // additive, element (b, h, i, j) at b*m_b_stride + h*m_h_stride + i*m_q_stride + j
+    long m_b_stride, m_h_stride, m_q_stride;
+    int mask_f32;                // 1: fp32 mask (added in fp32), 0: bf16 mask (sum rounded to bf16)
+    int B, Lq, Lk, H, Hkv, hd;
+    float scale;
+    int scale_div;               // 1: s / scale (Gemma's "/ math.sqrt(head_dim)"), 0: s * scale (SigLIP)
+};
+size_t attention_exact_lds(int Lk, int hd);
+void attention_exact(hipStream_t s, const ModAttnArgs& a);
+// apply_rotary_pos_emb on one projection: x (rows, heads*hd), cos/sin (rows, hd) bf16
+void rope_rows(hipStream_t s, const uint16_t* x, const uint16_t* cs, const uint16_t* sn, long rows, int heads, int hd,
+               uint16_t* out);
+
 // ---------------------------------------------------------------- misc
 // Fused consumer of a projection + residual: if split > 1, h = bf16(bf16(sum_z ws[z] (+bias)) + h)
 // (fixed z order) is written back to h first; then out = norm(h): RMSNorm (b == nullptr,

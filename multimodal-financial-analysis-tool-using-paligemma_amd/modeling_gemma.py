@@ -137,13 +137,6 @@ class PaliGemmaConfig:
         self.vision_config.projection_dim = projection_dim
 
 
-def _fused(name):
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError(f"{name}.forward is fused into libpgmi; call GemmaForCausalLM or "
-                                  "PaliGemmaForConditionalGeneration instead")
-    return forward
-
-
 class GemmaRMSNorm(nn.Module):
     """modeling_gemma.py:107-120 (weight applied as (1 + w))."""
 
@@ -242,7 +235,9 @@ class GemmaAttention(nn.Module):
         self.rotary_emb = GemmaRotaryEmbedding(self.head_dim, max_position_embeddings=self.max_position_embeddings,
                                                base=self.rope_theta)
 
-    forward = _fused("GemmaAttention")
+    # callable on its own (pgmi/modules.py: q/k/v GEMMs, the module's rotary_emb + pgmi_op_rope,
+    # kv_cache.update, pgmi_op_attention_ex with the mask, o_proj); returns (out, attn_weights)
+    forward = _modules.gemma_attention_forward
 
 
 class GemmaDecoderLayer(nn.Module):
@@ -256,7 +251,7 @@ class GemmaDecoderLayer(nn.Module):
         self.input_layernorm = GemmaRMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.post_attention_layernorm = GemmaRMSNorm(config.hidden_size, eps=config.rms_norm_eps)
 
-    forward = _fused("GemmaDecoderLayer")
+    forward = _modules.gemma_decoder_layer_forward  # calls its submodules as modules (hooks fire)
 
 
 class GemmaModel(nn.Module):
@@ -274,7 +269,9 @@ class GemmaModel(nn.Module):
     def get_input_embeddings(self):
         return self.embed_tokens
 
-    forward = _fused("GemmaModel")
+    # callable on its own, layer by layer through the module forwards (GemmaForCausalLM and
+    # PaliGemmaForConditionalGeneration run the fused engine instead)
+    forward = _modules.gemma_model_forward
 
 
 def _positions_2d(position_ids, B, L) -> torch.Tensor:

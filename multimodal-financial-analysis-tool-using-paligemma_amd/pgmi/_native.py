@@ -89,6 +89,10 @@ SIGNATURES = {
     "pgmi_op_add": (i32, [vp, vp, vp, i64, vp, vp]),
     "pgmi_op_patch_embed": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
     "pgmi_op_gemv_res": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
+    "pgmi_op_attention_ex": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, i32, vp, i32, i64, i64,
+                                   i64, vp, vp]),
+    "pgmi_op_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, vp, vp]),
+    "pgmi_op_scale": (i32, [vp, vp, f32, i64, vp, vp]),
 }
 
 _lib = None

@@ -1,6 +1,6 @@
-"""Per-layer module forwards of the drop-in model (SigLIP layers, GemmaRMSNorm, GemmaMLP) on libpgmi's
-single-op C-ABI entries (include/pgmi.h: pgmi_op_gemm / _layernorm / _rmsnorm / _attention / _add /
-_patch_embed).
+"""Per-layer module forwards of the drop-in model (SigLIP layers; GemmaRMSNorm, GemmaMLP, GemmaAttention,
+GemmaDecoderLayer, GemmaModel) on libpgmi's single-op C-ABI entries (include/pgmi.h: pgmi_op_gemm /
+_layernorm / _rmsnorm / _attention / _attention_ex / _rope / _add / _scale / _patch_embed).
 
 The whole-model forwards (PaliGemmaForConditionalGeneration, SiglipVisionModel, GemmaForCausalLM) run
 the fused engine and never call these; they exist so that a submodule called on its own -- and any
@@ -10,10 +10,17 @@ modeling_gemma.py:107-134), with the reference's bf16 rounding points:
   * fc1 + gelu(tanh)         -> bf16(gelu(bf16(acc + bias)))            (epilogue 2)
   * gate/up + GeGLU          -> bf16(bf16(gelu(bf16(g))) * bf16(u))     (epilogue 7, gate|up rows stacked)
   * residual adds            -> bf16(a + b)                             (pgmi_op_add)
-Every op runs on a small per-device context of its own (weights are passed by pointer); inputs and
-parameters are bf16 on the GPU (other float dtypes are rounded to bf16, as the fused path does).
+  * rotary                   -> bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)) (pgmi_op_rope)
+  * attention                -> bf16(q.k), bf16(* scale | / sqrt(hd)), bf16(+ mask), bf16(softmax_fp32),
+                                bf16(p.v); the probabilities are returned as the reference returns them
+                                (pgmi_op_attention_ex)
+Every op runs on a small context of its own per (device, stream) -- the context's scratch holds split-K
+partials, so two streams never share one (weights are passed by pointer); inputs and parameters are bf16
+on the GPU (other float dtypes are rounded to bf16, as the fused path does).
 """
 from __future__ import annotations
+
+import math
 
 import torch
 
@@ -25,15 +32,18 @@ _CTX = {}
 
 
 def _ctx(device: torch.device) -> Engine:
-    """Per-device context for the single-op entries (a zero-layer model: only its scratch is used)."""
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    """Context for the single-op entries on (device, current stream): a zero-layer model whose scratch
+    (split-K partials, patch-embedding staging, attention partials) is used from offset 0 by every op,
+    so ops issued on different streams get different contexts and never overwrite each other's."""
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     e = _CTX.get(key)
     if e is None:
         from .binding import _DUMMY_TEXT, _DUMMY_VISION
         from .synthetic import init_policy
         cfg = {"vision_config": dict(_DUMMY_VISION), "text_config": dict(_DUMMY_TEXT), "image_token_index": 7,
                "projection_dim": 2048, "pad_token_id": None}
-        e = Engine(cfg, device=torch.device("cuda", key), max_batch=1, max_seq=64, max_kv=64)
+        e = Engine(cfg, device=torch.device("cuda", dev), max_batch=1, max_seq=64, max_kv=64)
         e.fill_synthetic(0, init_policy)
         e.prepare()
         _CTX[key] = e
@@ -107,6 +117,56 @@ def attention(q, k, v, n_heads: int, n_kv: int, head_dim: int, scale: float) -> 
     return out
 
 
+def attention_ex(q, k, v, n_heads: int, n_kv: int, head_dim: int, scale: float, scale_div: bool = False,
+                 kv_layout: int = 0, mask=None):
+    """Reference-order attention returning (o, probs): q (B, Lq, H*hd) rows; k/v (B, Lk, Hkv*hd) rows
+    (kv_layout 0) or (B, Hkv, Lk, hd) (kv_layout 1, the KVCache layout); mask additive, broadcastable
+    to (B, H, Lq, Lk) -> o (B, Lq, H*hd), probs (B, H, Lq, Lk) bf16."""
+    qs, ks, vs = _bf(q), _bf(k), _bf(v)
+    B, Lq = qs.shape[0], qs.shape[1]
+    Lk = ks.shape[1] if kv_layout == 0 else ks.shape[2]
+    out = torch.empty((B, Lq, n_heads * head_dim), dtype=torch.bfloat16, device=qs.device)
+    probs = torch.empty((B, n_heads, Lq, Lk), dtype=torch.bfloat16, device=qs.device)
+    mp, mdt, ms = None, N.DTYPE_BF16, (0, 0, 0)
+    if mask is not None:
+        m = torch.as_tensor(mask, device=qs.device)
+        if m.dtype not in (torch.bfloat16, torch.float32):
+            m = m.float()                                   # torch promotes bf16 + (fp16 | fp64) past bf16
+        m = m.broadcast_to((B, n_heads, Lq, Lk))
+        if m.stride(-1) != 1:
+            m = m.contiguous()
+        mp, mdt, ms = m, (N.DTYPE_F32 if m.dtype == torch.float32 else N.DTYPE_BF16), m.stride()[:3]
+    e = _ctx(qs.device)
+    N.check(e.lib.pgmi_op_attention_ex(e.ctx, qs.data_ptr(), ks.data_ptr(), vs.data_ptr(), out.data_ptr(), B, Lq, Lk,
+                                       n_heads, n_kv, head_dim, kv_layout, float(scale), int(bool(scale_div)),
+                                       N.ptr(mp), mdt, ms[0], ms[1], ms[2], probs.data_ptr(),
+                                       N.stream_handle(qs.device)), "pgmi_op_attention_ex")
+    return out, probs
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, heads: int, head_dim: int) -> torch.Tensor:
+    """apply_rotary_pos_emb on one projection: x (B, L, heads*hd), cos/sin broadcastable to (B, L, hd)."""
+    xs = _bf(x)
+    B, L = xs.shape[0], xs.shape[1]
+    c = _bf(cos.broadcast_to((B, L, head_dim)))
+    s_ = _bf(sin.broadcast_to((B, L, head_dim)))
+    out = torch.empty_like(xs)
+    e = _ctx(xs.device)
+    N.check(e.lib.pgmi_op_rope(e.ctx, xs.data_ptr(), c.data_ptr(), s_.data_ptr(), B * L, heads, head_dim,
+                               out.data_ptr(), N.stream_handle(xs.device)), "pgmi_op_rope")
+    return out
+
+
+def scale(x: torch.Tensor, a: float) -> torch.Tensor:
+    """bf16(x * a), a already in the reference's precision (GemmaModel's bf16 normalizer)."""
+    xs = _bf(x)
+    out = torch.empty_like(xs)
+    e = _ctx(xs.device)
+    N.check(e.lib.pgmi_op_scale(e.ctx, xs.data_ptr(), float(a), xs.numel(), out.data_ptr(), N.stream_handle(xs.device)),
+            "pgmi_op_scale")
+    return out
+
+
 # ---------------------------------------------------------------- module forwards
 
 def siglip_embeddings_forward(self, pixel_values: torch.FloatTensor) -> torch.Tensor:
@@ -129,13 +189,13 @@ def siglip_embeddings_forward(self, pixel_values: torch.FloatTensor) -> torch.Te
 
 
 def siglip_attention_forward(self, hidden_states: torch.Tensor):
-    """SiglipAttention.forward (modeling_siglip.py:97-147).  Returns (attn_output, None): the fused
-    attention never materialises the (B, H, L, L) probability matrix the reference also returns."""
+    """SiglipAttention.forward (modeling_siglip.py:97-147): (attn_output, attn_weights), the
+    probabilities (B, H, L, L) bf16 as the reference returns them (:125,147)."""
     q = linear(hidden_states, self.q_proj.weight, self.q_proj.bias, EPI_BIAS)
     k = linear(hidden_states, self.k_proj.weight, self.k_proj.bias, EPI_BIAS)
     v = linear(hidden_states, self.v_proj.weight, self.v_proj.bias, EPI_BIAS)
-    o = attention(q, k, v, self.num_heads, self.num_heads, self.head_dim, self.scale)
-    return linear(o, self.out_proj.weight, self.out_proj.bias, EPI_BIAS), None
+    o, probs = attention_ex(q, k, v, self.num_heads, self.num_heads, self.head_dim, self.scale)
+    return linear(o, self.out_proj.weight, self.out_proj.bias, EPI_BIAS), probs
 
 
 def siglip_mlp_forward(self, hidden_states: torch.Tensor) -> torch.Tensor:
@@ -183,3 +243,57 @@ def gemma_mlp_forward(self, x: torch.Tensor) -> torch.Tensor:
         gu = torch.cat([_bf(g), _bf(u)], 0)
     act = linear(x, gu, None, EPI_GEGLU)
     return linear(act, self.down_proj.weight, None, EPI_STORE)
+
+
+def _proj(x, lin):
+    return linear(x, lin.weight, lin.bias, EPI_BIAS if lin.bias is not None else EPI_STORE)
+
+
+def gemma_attention_forward(self, hidden_states: torch.Tensor, attention_mask=None, position_ids=None,
+                            kv_cache=None, **kwargs):
+    """GemmaAttention.forward (modeling_gemma.py:231-293): q/k/v projections, the module's own
+    rotary_emb (monkey-patchable, ablation_study_fixed.py:144-166) applied by pgmi_op_rope,
+    kv_cache.update (:258-259), repeat_kv folded into the attention's head mapping, the additive
+    mask, o_proj.  Returns (attn_output, attn_weights)."""
+    bsz, q_len, _ = hidden_states.size()
+    H, Hkv, hd = self.num_heads, self.num_key_value_heads, self.head_dim
+    q = _proj(hidden_states, self.q_proj)
+    k = _proj(hidden_states, self.k_proj)
+    v = _proj(hidden_states, self.v_proj)
+    value_states = v.view(bsz, q_len, Hkv, hd).transpose(1, 2)
+    cos, sin = self.rotary_emb(value_states, position_ids, seq_len=None)   # (B|1, L, hd)
+    q = rope(q, cos, sin, H, hd)
+    k = rope(k, cos, sin, Hkv, hd)
+    key_states = k.view(bsz, q_len, Hkv, hd).transpose(1, 2)
+    if kv_cache is not None:
+        key_states, value_states = kv_cache.update(key_states, value_states, self.layer_idx)
+    assert attention_mask is not None                                      # :268
+    o, probs = attention_ex(q, key_states.contiguous(), value_states.contiguous(), H, Hkv, hd, math.sqrt(hd),
+                            scale_div=True, kv_layout=1, mask=attention_mask)
+    if o.size() != (bsz, q_len, H * hd):
+        raise ValueError(f" attn_output should be of size {(bsz, H, q_len, hd)}, but is {tuple(o.shape)}")
+    return _proj(o, self.o_proj), probs
+
+
+def gemma_decoder_layer_forward(self, hidden_states=None, attention_mask=None, position_ids=None, kv_cache=None):
+    """GemmaDecoderLayer.forward (modeling_gemma.py:307-338): the submodules are called as modules,
+    so their forward hooks fire as in the reference."""
+    residual = hidden_states
+    h = self.input_layernorm(hidden_states)
+    h, _ = self.self_attn(hidden_states=h, attention_mask=attention_mask, position_ids=position_ids, kv_cache=kv_cache)
+    h = add(residual, h)
+    residual = h
+    h = self.post_attention_layernorm(h)
+    h = self.mlp(h)
+    return add(residual, h)
+
+
+def gemma_model_forward(self, attention_mask=None, position_ids=None, inputs_embeds=None, kv_cache=None):
+    """GemmaModel.forward (modeling_gemma.py:357-382): x bf16(sqrt(hidden)) (:367-368, the normalizer
+    rounded to the embeddings' dtype as torch.tensor(..., dtype=...) does), the layers, the final norm."""
+    h = inputs_embeds
+    normalizer = float(torch.tensor(self.config.hidden_size ** 0.5, dtype=torch.bfloat16))
+    h = scale(h, normalizer)
+    for decoder_layer in self.layers:
+        h = decoder_layer(h, attention_mask=attention_mask, position_ids=position_ids, kv_cache=kv_cache)
+    return self.norm(h)

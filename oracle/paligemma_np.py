@@ -16,12 +16,30 @@ import math
 import numpy as np
 
 F32 = np.float32
+_FP32_TRUTH = [False]
+
+
+class fp32_truth:
+    """Context manager: every bf16 rounding point becomes the identity, i.e. the reference run
+    with its modules in float32 on the same (bf16-valued) weights -- how make_golden.py produced
+    the full_*_fp32.npz truths.  Used to measure the reference bf16's own error floor on the
+    small configurations (smoke, tests/test_gpu_model_small.py)."""
+
+    def __enter__(self):
+        _FP32_TRUTH[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _FP32_TRUTH[0] = False
+        return False
 
 
 # ---------------------------------------------------------------- bf16 helpers
 def bf16(x) -> np.ndarray:
     """Round float32 -> bf16 (round-to-nearest-even), returned widened to float32."""
     x = np.ascontiguousarray(x, dtype=F32)
+    if _FP32_TRUTH[0]:
+        return x
     u = x.view(np.uint32)
     r = (u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) & np.uint32(0xFFFF0000)
     return r.view(F32)
@@ -95,8 +113,9 @@ def siglip_embeddings(P, cfg, pixel_values):
     return bf16(y + P[pre + "position_embedding.weight"][None])
 
 
-def siglip_attention(P, pre, x, n_heads):
-    """SiglipAttention.forward (modeling_siglip.py:97-147)."""
+def siglip_attention(P, pre, x, n_heads, taps=None):
+    """SiglipAttention.forward (modeling_siglip.py:97-147); taps["probs"] = the attention
+    probabilities the reference returns as its second output (:125,147)."""
     B, L, D = x.shape
     hd = D // n_heads
     q = linear(x, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"])
@@ -108,6 +127,8 @@ def siglip_attention(P, pre, x, n_heads):
     s = bf16(np.matmul(q, k.transpose(0, 1, 3, 2)))                # :116 matmul -> bf16
     s = bf16(s * F32(hd ** -0.5))                                    # :116 * scale -> bf16
     p = bf16(softmax_f32(s))                                         # :125
+    if taps is not None:
+        taps["probs"] = p
     o = bf16(np.matmul(p, vv))                                       # :131
     o = o.transpose(0, 2, 1, 3).reshape(B, L, D)                     # :140-142
     return linear(o, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])  # :145
@@ -198,8 +219,10 @@ class KV:
         return self.k[i], self.v[i]
 
 
-def gemma_attention(P, cfg, i, x, positions, kv, invf):
-    """GemmaAttention.forward (modeling_gemma.py:231-293), mask == 0 (non-causal)."""
+def gemma_attention(P, cfg, i, x, positions, kv, invf, mask=None, taps=None):
+    """GemmaAttention.forward (modeling_gemma.py:231-293).  mask: the additive attention mask
+    (:269, bf16-valued, broadcast to (B, H, Lq, Lk)); None = the all-zero mask the merge builds
+    (:506-511).  taps["probs"] = the probabilities the reference returns (:273,293)."""
     t = cfg["text_config"]
     NH, NKV, HD = t["num_attention_heads"], t["num_key_value_heads"], t.get("head_dim", 256)
     pre = f"language_model.model.layers.{i}.self_attn."
@@ -218,7 +241,11 @@ def gemma_attention(P, cfg, i, x, positions, kv, invf):
     v = np.repeat(v, rep, axis=1)
     s = bf16(np.matmul(q, k.transpose(0, 1, 3, 2)))                  # :266 matmul
     s = bf16(s / F32(math.sqrt(HD)))                                 # :266 / sqrt(d)
-    p = bf16(softmax_f32(s))                                         # :269-273 (+0 mask)
+    if mask is not None:
+        s = bf16(s + mask)                                           # :269
+    p = bf16(softmax_f32(s))                                         # :273
+    if taps is not None:
+        taps["probs"] = p
     o = bf16(np.matmul(p, v))                                        # :277
     o = o.transpose(0, 2, 1, 3).reshape(B, L, NH * HD)
     return linear(o, P[pre + "o_proj.weight"])                       # :291

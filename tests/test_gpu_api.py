@@ -142,13 +142,17 @@ def test_error_conventions(model, gold):
 
 
 def test_submodule_forwards(model):
-    """GemmaDecoderLayer / GemmaAttention stay fused into the engine (KV cache + RoPE in its kernels) and
-    raise; GemmaMLP / GemmaRMSNorm run on their own (tests/test_gpu_modules.py checks their values) --
-    here on the bound model, whose gate|up parameters are adjacent slab views read in place."""
+    """Every Gemma submodule runs on its own (tests/test_gpu_modules.py checks their values against the
+    oracle) -- here on the bound model, whose parameters are slab views read in place (gate|up adjacent).
+    GemmaAttention asserts a mask as the reference does (modeling_gemma.py:268)."""
     layer = model.language_model.model.layers[0]
     x = torch.randn(1, 3, 2048, device="cuda").bfloat16()
-    with pytest.raises(NotImplementedError):
-        layer(x)
+    mask = torch.zeros(1, 1, 3, 3, dtype=torch.bfloat16, device="cuda")
+    pos = torch.arange(3, device="cuda")[None]
+    y = layer(x, attention_mask=mask, position_ids=pos)
+    assert y.shape == (1, 3, 2048) and y.dtype == torch.bfloat16 and bool(torch.isfinite(y.float()).all())
+    with pytest.raises(AssertionError):
+        layer.self_attn(hidden_states=x, attention_mask=None, position_ids=pos)
     y = layer.mlp(x)
     assert y.shape == (1, 3, 2048) and y.dtype == torch.bfloat16 and bool(torch.isfinite(y.float()).all())
     z = layer.input_layernorm(x)

@@ -6,6 +6,9 @@ sec.8c):
   * |our logit - reference logit| <= 0.25 at the reference's top-8 tokens of every step;
   * our bf16 error vs the fp32 reference is <= 1.5x the reference-bf16 error vs fp32
     (rel-L2 over the 1024 sampled vocabulary entries, averaged over the 64 steps);
+  * per-step rel-L2 vs the reference bf16 <= 2e-2, or where the reference bf16 is itself further
+    from its fp32 truth, <= 1.6x that step's reference error (mean over the steps <= 1.25x the
+    reference's mean error): tests_helpers.assert_step_rule, measured table in DESIGN.md sec.5;
   * free-running greedy tokens equal the reference's up to the first low-margin step.
 """
 import os
@@ -15,15 +18,10 @@ import pytest
 import torch
 
 from oracle import weights as W
-from tests_helpers import pixels_from_u8
+from tests_helpers import check_model_parity, logit_stats, pixels_from_u8
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 SEED = 1234
-
-
-def rel(a, b):
-    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
-    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
 @pytest.fixture(scope="module")
@@ -76,13 +74,9 @@ def _teacher_forced(e, G, gb, gf, n):
     am = ours.argmax(-1).cpu().numpy()
     decisive = gb["margin"] > 0.25
     assert np.array_equal(am[decisive], ref_toks[decisive]), (am, ref_toks)
-    # error vs fp32 truth relative to the reference's own bf16 error
-    err_ours = np.mean([rel(ours_s[t], gf["sample_vals"][t]) for t in range(n)])
-    err_ref = np.mean([rel(gb["sample_vals"][t], gf["sample_vals"][t]) for t in range(n)])
-    assert err_ours <= 1.5 * err_ref, (err_ours, err_ref)
-    # closeness to the reference bf16 itself, on average and at every step
-    per_step = [rel(ours_s[t], gb["sample_vals"][t]) for t in range(n)]
-    assert np.mean(per_step) < 3e-2 and max(per_step) < 6e-2, (np.mean(per_step), max(per_step))
+    # per-step closeness to the reference bf16 (against its own fp32 floor) and our
+    # error vs the fp32 truth relative to the reference's own bf16 error
+    check_model_parity(f"full224/teacher_forced_{n}", ours_s, gb["sample_vals"][:n], gf["sample_vals"][:n])
 
 
 @torch.no_grad()
@@ -146,7 +140,10 @@ def test_prefill_448(G):
         top = torch.gather(lg, 0, torch.from_numpy(g["topk_idx"][0]).cuda()).cpu().numpy()
         assert np.abs(top - g["topk_val"][0]).max() <= 0.25, rows
         s = lg[torch.from_numpy(g["sample_idx"]).cuda()].cpu().numpy()
-        assert rel(s, g["sample_vals"][0]) < 3e-2, rows
+        # no fp32 truth exists for the 448 px fixture: the 224 px floor (2.4e-2 at the prefill
+        # step) is what the 3e-2 bound covers
+        st = logit_stats(f"full448/prefill_rows{rows}", s[None], g["sample_vals"][:1])
+        assert st["rel_vs_ref_bf16_max"] < 3e-2, rows
         if g["margin"][0] > 0.25:
             assert int(lg.argmax()) == int(g["topk_idx"][0, 0]), rows
     del e

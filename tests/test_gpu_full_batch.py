@@ -7,9 +7,11 @@ alone; the reference cannot batch, processing_paligemma.py:80 / modeling_gemma.p
 Rules per row (as tests/test_gpu_full.py applies them to image 0):
   * teacher-forced on the row's reference tokens: |delta| <= 0.25 at the reference's top-8 of
     every step, argmax equal wherever the reference's top-2 margin exceeds 0.25, sampled-logit
-    rel-L2 < 3e-2 on average over the 64 steps, and the row's error vs its fp32 truth
-    (tests/golden/full_batch8_fp32.npz: the reference in fp32, teacher-forced on that row's token
-    path) <= 1.5x the reference bf16's own error vs that truth;
+    rel-L2 vs the row's reference bf16 <= 2e-2 per step, or <= 1.6x the reference bf16's own
+    error vs the row's fp32 truth at that step where that is larger (mean <= 1.25x; DESIGN.md
+    sec.5), and the row's error vs its fp32 truth (tests/golden/full_batch8_fp32.npz: the
+    reference in fp32, teacher-forced on that row's token path) <= 1.5x the reference bf16's own
+    error vs that truth;
   * free-running batched greedy: a row's first divergence sits on a step where its reference is
     indecisive (margin < 0.25).
 """
@@ -20,16 +22,11 @@ import pytest
 import torch
 
 from oracle import weights as W
-from tests_helpers import pixels_from_u8
+from tests_helpers import check_model_parity, pixels_from_u8
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 SEED = 1234
 N_STEPS = 64
-
-
-def rel(a, b):
-    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
-    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
 @pytest.fixture(scope="module")
@@ -83,11 +80,7 @@ def test_batch_rows_teacher_forced_vs_own_reference(eng, G, F, B):
         decisive = G["margin"][b] > 0.25
         assert np.array_equal(am[decisive], ref_toks[b][decisive]), (b, am, ref_toks[b])
         s = ours[b][:, sidx].cpu().numpy()
-        err = np.mean([rel(s[t], G["sample_vals"][b, t]) for t in range(N_STEPS)])
-        assert err < 3e-2, (b, err)
-        err_ours = np.mean([rel(s[t], F["sample_vals"][b, t]) for t in range(N_STEPS)])
-        err_ref = np.mean([rel(G["sample_vals"][b, t], F["sample_vals"][b, t]) for t in range(N_STEPS)])
-        assert err_ours <= 1.5 * err_ref, (b, err_ours, err_ref)
+        check_model_parity(f"batch{B}/row{b}", s, G["sample_vals"][b], F["sample_vals"][b])
 
 
 @pytest.mark.parametrize("B", [3, 8])

@@ -9,6 +9,7 @@ import torch
 
 from oracle import paligemma_np as O
 from oracle import weights as W
+from tests_helpers import check_model_parity, logit_stats
 
 pytestmark = pytest.mark.gpu
 SEED = 1234
@@ -34,6 +35,17 @@ def eng():
     return e
 
 
+@pytest.fixture(scope="module")
+def truth_last(gold):
+    """The oracle with every bf16 rounding point removed (O.fp32_truth: the reference in fp32 on the
+    same bf16-valued weights) -- the floor of the SURVEY sec.8c rule on this configuration."""
+    P = W.synthetic_state_dict_f32(W.small_config(), SEED)
+    with O.fp32_truth():
+        lg, _ = O.paligemma_prefill(P, W.small_config(), gold["ids"], O.from_bits(gold["pixels_bits"]),
+                                    all_logits=False)
+    return lg[:, -1]
+
+
 def tap(gold, name):
     return O.from_bits(gold["tap_" + name])
 
@@ -46,7 +58,7 @@ def test_vision_tower(eng, gold):
     assert rel_l2(proj[:, ::8], tap(gold, "image_features")) < 1.5e-2
 
 
-def test_prefill_logits(eng, gold):
+def test_prefill_logits(eng, gold, truth_last):
     px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
     ids = torch.from_numpy(gold["ids"]).cuda()
     L = ids.shape[1]
@@ -56,8 +68,11 @@ def test_prefill_logits(eng, gold):
     torch.cuda.synchronize()
     lg = logits.cpu().numpy()
     ref_last = gold["prefill_logits_last"]
-    assert rel_l2(lg[:, -1], ref_last) < 3e-2
-    assert rel_l2(lg[:, ::32], O.from_bits(gold["prefill_logits_rows"])) < 3e-2
+    # SURVEY sec.8c per-step rule against the reference bf16, with its own error vs fp32 as floor
+    check_model_parity("small/prefill_last", lg[:, -1], ref_last, truth_last)
+    # every 32nd row (no fp32 truth for the other rows: the last row's floor is what 3e-2 covers)
+    st = logit_stats("small/prefill_rows", lg[0, ::32], O.from_bits(gold["prefill_logits_rows"])[0])
+    assert st["rel_vs_ref_bf16_max"] < 3e-2
     # last-row-only mode (decode GEMV kernel) gives the same numbers up to reassociation
     kv2 = eng.new_kv(1, 1024)
     last = eng.lm_forward(kv2, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)
@@ -310,8 +325,9 @@ def test_decode_past_768_keys_vs_oracle(B):
     its two-pass form (gemv_body.h, > 12 chunks of 64 keys); B >= 3 decodes on the MFMA path with
     the k_attn_combine kernel.  A ~1000-token text prompt is prefilled, then 4 decode steps are
     teacher-forced along the oracle's greedy tokens and compared row by row (same rules as the
-    other model-level tests: rel-L2 < 3e-2, |delta| <= 0.25 at the oracle's top-8, argmax where
-    the oracle's top-2 margin exceeds 0.25)."""
+    other model-level tests: the per-step rel-L2 rule against the oracle bf16 with the oracle's fp32
+    truth as floor, |delta| <= 0.25 at the oracle's top-8, argmax where the oracle's top-2 margin
+    exceeds 0.25)."""
     from pgmi import Engine
     cfg = W.small_config()
     L, steps = 1000, 4
@@ -326,13 +342,18 @@ def test_decode_past_768_keys_vs_oracle(B):
     emb = O.merge(P, cfg, None, ids)
     okv = O.KV()
     ref = O.gemma_forward(P, cfg, emb, np.broadcast_to(np.arange(L), (B, L)), okv, all_logits=False)[:, -1]
+    # the fp32 truth along the same (oracle-bf16 greedy) tokens: the floor of the per-step rule
+    fkv = O.KV()
+    with O.fp32_truth():
+        tru = O.gemma_forward(P, cfg, emb, np.broadcast_to(np.arange(L), (B, L)), fkv, all_logits=False)[:, -1]
     kv = e.new_kv(B, L + 64)
     got = e.lm_forward(kv, 0, torch.arange(L)[None], ids=torch.from_numpy(ids).cuda(), logits_rows=1)[:, 0]
     logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device="cuda")
+    hist = []
     for t in range(steps + 1):
         g = got.cpu().numpy()
+        hist.append((g, ref, tru))
         for b in range(B):
-            assert rel_l2(g[b], ref[b]) < 3e-2, (t, b, rel_l2(g[b], ref[b]))
             top = np.argsort(ref[b])[-8:]
             assert np.abs(g[b][top] - ref[b][top]).max() <= 0.25, (t, b)
             s = np.sort(ref[b])
@@ -342,7 +363,12 @@ def test_decode_past_768_keys_vs_oracle(B):
             break
         nxt = ref.argmax(-1)                               # teacher-forced on the oracle's tokens
         ref = O.paligemma_decode(P, cfg, nxt, okv, L + 1 + t)[:, -1]
+        with O.fp32_truth():
+            tru = O.paligemma_decode(P, cfg, nxt, fkv, L + 1 + t)[:, -1]
         got = e.decode(torch.from_numpy(nxt).cuda(), kv, L + t, L + 1 + t, logits=logits, graph=t > 0).clone()
+    for b in range(B):
+        check_model_parity(f"small/decode_past_768_B{B}/row{b}", np.stack([h[0][b] for h in hist]),
+                           np.stack([h[1][b] for h in hist]), np.stack([h[2][b] for h in hist]))
     del e
     torch.cuda.empty_cache()
 

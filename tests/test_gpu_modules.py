@@ -57,8 +57,11 @@ def test_siglip_attention_and_mlp(setup):
     pre = "vision_tower.vision_model.encoder.layers.0."
     x = _x(np.random.default_rng(2), 2, 256, 1152)
     out, weights = layer.self_attn(hidden_states=torch.from_numpy(x).cuda().bfloat16())
-    assert weights is None
-    assert rel_l2(np32(out), O.siglip_attention(P, pre + "self_attn.", x, 16)) < 1e-2
+    taps = {}
+    assert rel_l2(np32(out), O.siglip_attention(P, pre + "self_attn.", x, 16, taps)) < 1e-2
+    # the probabilities the reference returns as its second output (modeling_siglip.py:125,147)
+    assert weights.shape == (2, 16, 256, 256) and weights.dtype == torch.bfloat16
+    assert rel_l2(np32(weights), taps["probs"]) < 1e-2
     h = layer.mlp(torch.from_numpy(x).cuda().bfloat16())
     assert rel_l2(np32(h), O.siglip_mlp(P, pre + "mlp.", x)) < 1e-2
 
@@ -126,3 +129,117 @@ def test_gemma_rmsnorm_and_mlp(setup):
         got = mlp(torch.from_numpy(x).cuda().bfloat16())
         assert got.shape == (3, 40, 2048)
         assert rel_l2(np32(got), ref) < 1e-2, adjacent
+
+
+# ---------------------------------------------------------------- Gemma layer modules
+def _gemma_layer(P, cfg, i=0):
+    import modeling_gemma as MG
+    gc = MG.GemmaConfig(**cfg["text_config"])
+    layer = MG.GemmaDecoderLayer(gc, i)
+    with torch.no_grad():
+        for name, p in layer.named_parameters():
+            p.data = torch.from_numpy(P[f"language_model.model.layers.{i}." + name]).to("cuda", torch.bfloat16)
+    return layer.cuda()
+
+
+@torch.no_grad()
+def test_gemma_attention_vs_oracle(setup):
+    """GemmaAttention.forward (modeling_gemma.py:231-293) on its own: zero mask, causal mask, and a KV
+    cache filled by a prefill then extended by one decode token (KVCache.update, :258-259); outputs
+    and the returned probabilities against the oracle."""
+    import modeling_gemma as MG
+    cfg, P, _ = setup
+    attn = _gemma_layer(P, cfg).self_attn
+    invf = O.inv_freq(256)
+    B, L = 2, 40
+    x = _x(np.random.default_rng(8), B, L, 2048) * 2
+    pos = np.broadcast_to(np.arange(L), (B, L))
+    xt, post = torch.from_numpy(x).cuda().bfloat16(), torch.from_numpy(pos.copy()).cuda()
+    # zero mask (the merge's, modeling_gemma.py:506-511)
+    zero = torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda")
+    out, w = attn(hidden_states=xt, attention_mask=zero, position_ids=post)
+    taps = {}
+    ref = O.gemma_attention(P, cfg, 0, x, pos, None, invf, taps=taps)
+    assert rel_l2(np32(out), ref) < 1e-2
+    assert w.shape == (B, 8, L, L) and rel_l2(np32(w), taps["probs"]) < 1e-2
+    # a causal additive mask (bf16 large negative above the diagonal)
+    cm = np.triu(np.full((L, L), -1e4, np.float32), 1)
+    cmask = torch.from_numpy(cm).to("cuda", torch.bfloat16)[None, None].expand(B, 1, L, L)
+    out, w = attn(hidden_states=xt, attention_mask=cmask, position_ids=post)
+    taps = {}
+    ref = O.gemma_attention(P, cfg, 0, x, pos, None, invf, mask=O.bf16(cm)[None, None], taps=taps)
+    assert rel_l2(np32(out), ref) < 1e-2
+    assert rel_l2(np32(w), taps["probs"]) < 1e-2
+    assert float(w[0, 0, 0, 1:].float().abs().max()) == 0.0
+    # KV cache: prefill L tokens, then one decode token at position L (the cache grows to L + 1)
+    kv, okv = MG.KVCache(), O.KV()
+    attn(hidden_states=xt, attention_mask=zero, position_ids=post, kv_cache=kv)
+    O.gemma_attention(P, cfg, 0, x, pos, okv, invf)
+    x1 = _x(np.random.default_rng(9), B, 1, 2048) * 2
+    p1 = np.full((B, 1), L)
+    out, w = attn(hidden_states=torch.from_numpy(x1).cuda().bfloat16(),
+                  attention_mask=torch.zeros(B, 1, 1, L + 1, dtype=torch.bfloat16, device="cuda"),
+                  position_ids=torch.from_numpy(p1).cuda(), kv_cache=kv)
+    assert kv.num_items() == L + 1 and kv.key_cache[0].shape == (B, 1, L + 1, 256)
+    ref = O.gemma_attention(P, cfg, 0, x1, p1, okv, invf)
+    assert rel_l2(np32(out), ref) < 1e-2
+    assert rel_l2(np32(kv.key_cache[0]), okv.k[0]) < 1e-2
+
+
+@torch.no_grad()
+def test_gemma_decoder_layer_hooks_and_model(setup):
+    """GemmaDecoderLayer.forward (modeling_gemma.py:307-338) runs its submodules as modules (their
+    forward hooks fire in the reference's order) and GemmaModel.forward (:357-382) -- normalizer,
+    the layers, the final norm -- against the oracle."""
+    import modeling_gemma as MG
+    cfg, P, _ = setup
+    gc = MG.GemmaConfig(**cfg["text_config"])
+    model = MG.GemmaModel(gc)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            p.data = torch.from_numpy(P["language_model.model." + name]).to("cuda", torch.bfloat16)
+    model = model.cuda()
+    layer = model.layers[0]
+    seen = []
+    hs = [m.register_forward_hook(lambda m, i, o, n=n: seen.append(n))
+          for n, m in (("ln1", layer.input_layernorm), ("attn", layer.self_attn), ("ln2", layer.post_attention_layernorm),
+                       ("mlp", layer.mlp), ("layer", layer), ("norm", model.norm))]
+    B, L = 1, 33
+    emb = _x(np.random.default_rng(10), B, L, 2048) * 0.05
+    pos = np.broadcast_to(np.arange(L), (B, L))
+    try:
+        got = model(attention_mask=torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda"),
+                    position_ids=torch.from_numpy(pos.copy()).cuda(), inputs_embeds=torch.from_numpy(emb).cuda().bfloat16())
+    finally:
+        for h in hs:
+            h.remove()
+    assert seen == ["ln1", "attn", "ln2", "mlp", "layer", "norm"]
+    taps = {}
+    O.gemma_forward(P, cfg, emb, pos, O.KV(), taps=taps, all_logits=False)
+    ref = O.rms_norm(taps["text_layer0"], P["language_model.model.norm.weight"], 1e-6)
+    assert rel_l2(np32(got), ref) < 1e-2
+
+
+@torch.no_grad()
+def test_gemma_model_modules_equal_fused(setup):
+    """The module-by-module GemmaModel + tied lm_head equals GemmaForCausalLM's fused forward
+    (pgmi_lm_forward) on the same parameters and embeddings."""
+    import modeling_gemma as MG
+    cfg, P, _ = setup
+    gc = MG.GemmaConfig(**cfg["text_config"])
+    lm = MG.GemmaForCausalLM(gc)
+    with torch.no_grad():
+        for name, p in lm.named_parameters():
+            key = "language_model." + name
+            if key in P:
+                p.data = torch.from_numpy(P[key]).to("cuda", torch.bfloat16)
+    lm.tie_weights()
+    lm = lm.cuda()
+    B, L = 1, 48
+    emb = torch.from_numpy(_x(np.random.default_rng(11), B, L, 2048) * 0.05).cuda().bfloat16()
+    pos = torch.arange(L, device="cuda")[None]
+    staged = lm.model(attention_mask=torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda"), position_ids=pos,
+                      inputs_embeds=emb)
+    staged_logits = (staged.float() @ lm.lm_head.weight.float().T).bfloat16().float()
+    fused = lm(attention_mask=torch.ones(B, L, device="cuda"), position_ids=pos, inputs_embeds=emb)["logits"]
+    assert rel_l2(np32(staged_logits), np32(fused)) < 1e-2

@@ -51,6 +51,26 @@ def time_lm(eng, args, iters):
     return e0.elapsed_time(e1) * 1e3 / iters, out
 
 
+# a candidate is eligible only when its output matches the default plan's (a broken candidate,
+# e.g. one whose split leaves a K range unwritten, must not win on time alone)
+REL_TOL = 1e-2
+
+
+def rel_err(out, ref):
+    d = (out.float() - ref.float()).norm() / ref.float().norm().clamp_min(1e-30)
+    return float(d)
+
+
+def report(name, Mm, Nn, K, rows):
+    ok = sorted(r for r in rows if r[3] < REL_TOL)
+    bad = [r for r in rows if not r[3] < REL_TOL]
+    print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (rel {e:.2g})" for t, c, sp, e in ok[:8]),
+          flush=True)
+    if bad:
+        print(f"  REJECTED (rel-L2 vs the default plan >= {REL_TOL}): "
+              + ", ".join(f"c{c}/s{sp} ({e:.2g})" for t, c, sp, e in bad), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--target", default="vision", choices=["vision", "lm"])
@@ -102,12 +122,9 @@ def main():
                 for sp in splits:
                     N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, dual, c, sp))
                     t, out = time_lm(eng, args, a.iters)
-                    err = float((out - ref).abs().max())
-                    rows.append((t, c, sp, err))
+                    rows.append((t, c, sp, rel_err(out, ref)))
             N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, dual, -1, 0))
-            rows.sort()
-            print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (d {e:.2g})" for t, c, sp, e in rows[:8]),
-                  flush=True)
+            report(name, Mm, Nn, K, rows)
         return
     M = n_img * a.batch
     shapes = {"qkv": (M, 3456, 1152, [1, 2]), "out": (M, 1152, 1152, [1, 2, 3, 4, 6]),
@@ -135,12 +152,9 @@ def main():
                 t = time_tower(eng, px, a.iters)
                 out = eng.vision(px)
                 torch.cuda.synchronize()
-                err = float((out.float() - ref.float()).abs().max())
-                rows.append((t, c, sp, err))
+                rows.append((t, c, sp, rel_err(out, ref)))
         N.check(eng.lib.pgmi_tune_gemm_shape(Mm, Nn, K, 0, -1, 0))
-        rows.sort()
-        print(f"{name} {Mm}x{Nn}x{K}: " + ", ".join(f"c{c}/s{sp}: {t:.1f} (d {e:.2g})" for t, c, sp, e in rows[:8]),
-              flush=True)
+        report(name, Mm, Nn, K, rows)
 
 
 if __name__ == "__main__":

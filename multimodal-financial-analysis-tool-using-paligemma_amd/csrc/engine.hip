@@ -100,6 +100,7 @@ struct pgmi_ctx {
     size_t ws_bytes;
     // decode workspace
     uint16_t *dH, *dQ, *dAO, *dACT;
+    uint16_t* dHn;  // batched decode (B >= 3): the RMSNorm'd rows the unstaged MFMA projections read
     float *opart, *pmax, *dlogits, *amax_v;
     int *pidx, *amax_i;
     int max_chunks;
@@ -583,6 +584,7 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->dQ, (size_t)B * c.t_heads * c.t_head_dim))) return rc;
         if ((rc = dalloc_t(x, &x->dAO, (size_t)B * H))) return rc;
         if ((rc = dalloc_t(x, &x->dACT, (size_t)B * c.t_intermediate))) return rc;
+        if ((rc = dalloc_t(x, &x->dHn, (size_t)B * H))) return rc;
         x->max_chunks = (c.max_kv + 63) / 64;
         if ((rc = dalloc_t(x, &x->opart, attention_decode_part_floats(B, c.t_kv_heads, x->max_chunks)))) return rc;
         if ((rc = dalloc_t(x, &x->pmax, (size_t)B * gemv_logits_blocks()))) return rc;
@@ -902,6 +904,13 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
+// probe knob: PGMI_MF_STAGED=1 keeps the round-3 batched form (each projection stages and normalises its
+// rows itself) for same-box A/Bs
+static bool mf_staged() {
+    static const bool v = [] { const char* e = getenv("PGMI_MF_STAGED"); return e && atoi(e) != 0; }();
+    return v;
+}
+
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr) {
     const pgmi_config& c = x->c;
@@ -917,11 +926,17 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
     if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
     else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    // B >= 3 (MFMA projections): every RMSNorm is computed once per row (k_rows_norm after o_proj, fused
+    // into the down projection's combine for the next layer's input norm) and the q|k|v and gate|up
+    // projections read the normalised rows dHn without staging
+    const bool mf = B >= gemv_mf_min_batch() && !mf_staged();
+    if (mf && c.t_layers > 0) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-        gemv_qkv(s, B, NH, NKV, x->dH, TL(x, i, "input_layernorm.weight"), eps, TL(x, i, "self_attn.q_proj.weight"),
-                 x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws, (fold && i == 0) ? &emb : nullptr);
+        gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
+                 TL(x, i, "self_attn.q_proj.weight"), x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws,
+                 (fold && i == 0) ? &emb : nullptr);
         AttnArgs a{};
         a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -931,6 +946,13 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
                     B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+        if (mf) {
+            rows_norm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, B, H, x->dHn);
+            gemv_geglu(s, B, x->dHn, nullptr, eps, TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);
+            gemv_res_norm(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws,
+                          i + 1 < c.t_layers ? TL(x, i + 1, "input_layernorm.weight") : nullptr, eps, x->dHn);
+            continue;
+        }
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);

@@ -10,6 +10,7 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a);
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o);
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks);
 void gemv_mf_res(hipStream_t s, const GemvArgs& a, float* ws);
+void gemv_mf_res_norm(hipStream_t s, const GemvArgs& a, float* ws, const uint16_t* norm_w, float eps, uint16_t* hn);
 
 template <int B, int KCH, int RPW, int MODE, int WK = 1, int DEPTH = 1, bool EMB = false>
 static void launch_gemv(hipStream_t s, const GemvArgs& a, int max_blocks = 0) {
@@ -76,6 +77,20 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
             else launch_gemv<4, 32, 2, GV_RES, 4>(s, c);
         }
     }
+}
+
+// batched (MFMA) residual projection whose combine also writes the next RMSNorm of h (hn); other
+// batches / shapes: gemv_res, then rows_norm
+void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
+                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn) {
+    if (B >= gemv_mf_min_batch() && K % 2048 == 0 && K / 2048 <= 8 && K > 2048 && ws) {
+        GemvArgs a{};
+        a.x = x; a.norm_w = nullptr; a.W = W; a.n_units = N; a.K = K; a.nb = B; a.out = h_inout;
+        gemv_mf_res_norm(s, a, ws, norm_w, eps, hn);
+        return;
+    }
+    gemv_res(s, B, K, x, W, N, h_inout, ws);
+    if (norm_w) rows_norm(s, h_inout, norm_w, eps, B, N, hn);
 }
 
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,

@@ -17,6 +17,8 @@
 //     fused in, or read from global (o_proj's and down_proj's inputs);
 //   - epilogues and rounding points exactly as gemv_body.h (RoPE + KV append, GeGLU, residual,
 //     fp32 logits + per-workgroup first-max argmax partials).
+#include <cstdlib>
+
 #include "gemv_body.h"
 
 namespace pgmi {
@@ -99,10 +101,12 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
 // group multiplies -- two register buffers in ping-pong, every issue unconditional (groups past the
 // end read one 64-B line of the matrix: all lanes the same address, results discarded), so the
 // compiler's in-order vmcnt keeps the second stream in flight across the first's wait.
-template <int MODE, int NR, int KW, int WK, int PF = 1>
+// NS (no staging): the q|k|v / gate|up input is already RMSNorm'd (k_rows_norm / k_mf_combine_norm
+// wrote it), so each wave reads its K slice straight from global like the residual projections
+template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false>
 __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restrict__ ws) {
     constexpr int NKB = KW / 128;          // 128-wide k blocks per wave
-    constexpr bool STAGE = (MODE != GV_RES);
+    constexpr bool STAGE = (MODE != GV_RES) && !NS;
     extern __shared__ __attribute__((aligned(16))) uint16_t mfs[];
     __shared__ float red[MF_MAXB * 16];
     __shared__ f32x4 kred[WK][NR][64];
@@ -593,19 +597,101 @@ __global__ void k_mf_combine(const float* __restrict__ ws, int KS, int nb, int N
     h[i] = f2bf(rbf(s) + bf2f(h[i]));
 }
 
+// One workgroup per batch row: RMSNorm (modeling_gemma.py:114-120) of x -> out, the rows the
+// unstaged batched projections read.  Every thread's chunks are loaded before the reduction.
+__global__ void __launch_bounds__(256) k_rows_norm(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                   float eps, int K, uint16_t* __restrict__ out) {
+    __shared__ float red[4];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint16_t* xr = x + (long)b * K;
+    float ss = 0.f;
+    for (int c = tid * 8; c < K; c += 256 * 8) {
+        const uint4 v = ldg16(xr + c);
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float f = bf2f(e[j]); ss += f * f; }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    const float r = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+    for (int c = tid * 8; c < K; c += 256 * 8) {
+        const uint4 v = ldg16(xr + c), wv = ldg16(w + c);
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r) * (1.0f + bf2f(we[j])));
+        *reinterpret_cast<u16x8*>(out + (long)b * K + c) = o;
+    }
+}
+
+// k_mf_combine (KS <= 8) with the next RMSNorm fused: one workgroup per batch row, h = bf16(bf16(sum_ks ws[ks])
+// + h) (fixed ks order, the slab loads issued up front as k_mf_combine), then (w != nullptr) hn =
+// RMSNorm(h) -- the next layer's normalised input, so its q|k|v projection stages nothing
+__global__ void __launch_bounds__(256) k_mf_combine_norm(const float* __restrict__ ws, int KS, int N,
+                                                         uint16_t* __restrict__ h, const uint16_t* __restrict__ w,
+                                                         float eps, uint16_t* __restrict__ hn) {
+    __shared__ float red[4];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long slab = (long)gridDim.x * N;
+    float ss = 0.f;
+    for (int c = tid * 8; c < N; c += 256 * 8) {
+        const long i0 = (long)b * N + c;
+        f32x4 p[8][2];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const long o = (long)(q < KS ? q : 0) * slab + i0;
+            p[q][0] = *reinterpret_cast<const f32x4*>(ws + o);
+            p[q][1] = *reinterpret_cast<const f32x4*>(ws + o + 4);
+        }
+        const uint4 hv = ldg16(h + i0);
+        const uint16_t* he = reinterpret_cast<const uint16_t*>(&hv);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = p[0][j >> 2][j & 3];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) t = q < KS ? t + p[q][j >> 2][j & 3] : t;
+            o.v[j] = f2bf(rbf(t) + bf2f(he[j]));
+            const float f = bf2f(o.v[j]);
+            ss += f * f;
+        }
+        *reinterpret_cast<u16x8*>(h + i0) = o;
+    }
+    if (!w) return;
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    const float r = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
+    for (int c = tid * 8; c < N; c += 256 * 8) {
+        const uint4 v = ldg16(h + (long)b * N + c), wv = ldg16(w + c);  // this thread's own stores
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e[j]) * r) * (1.0f + bf2f(we[j])));
+        *reinterpret_cast<u16x8*>(hn + (long)b * N + c) = o;
+    }
+}
+
+void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, int nb, int K, uint16_t* out) {
+    hipLaunchKernelGGL(k_rows_norm, dim3(nb), dim3(256), 0, s, x, w, eps, K, out);
+}
+
 // smallest lock-step batch whose decode projections run on MFMA (B <= 2: the v_dot2 GEMVs of gemv_body.h)
 int gemv_mf_min_batch() { return 3; }
 
-template <int MODE, int NR, int KW, int WK, int PF = 1>
+template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false>
 static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
-    const size_t lds = (MODE == GV_RES) ? 0 : (size_t)a.nb * (a.K + 8) * sizeof(uint16_t);
+    const size_t lds = (MODE == GV_RES || NS) ? 0 : (size_t)a.nb * (a.K + 8) * sizeof(uint16_t);
     static size_t attr = 0;
     if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK, PF>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK, PF, NS>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK, PF>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
+    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK, PF, NS>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
 }
 
 static int groups_of(int units) { return (units + 15) / 16; }
@@ -635,7 +721,13 @@ static int ms_blocks(int units, int cap) {
 void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
     GemvArgs r = a;
     r.n_units = 2 * a.n_units;
-    launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
+    if (a.norm_w) launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
+    else launch_mf<GV_QKV, 1, 256, 8, 1, true>(s, r, groups_of(r.n_units), 1, nullptr);  // input already normed
+}
+
+static int mf_gu_blocks() {
+    const char* e = getenv("PGMI_MF_GU_BLOCKS");  // probe knob (same-box sweeps of the unstaged form)
+    return e ? atoi(e) : 512;
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
@@ -644,7 +736,8 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
     // (tools/b8_ab.sh) B = 8 step 1.737 -> 1.681 ms against the one-workgroup-per-CU LDS-DMA ring
     // (k_gemv_ml, 4 waves x 3-deep rings); 256 / 384 / 1,024 workgroups and 2 or 8 K-split waves
     // measured slower (1.746-2.051 ms)
-    launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
+    if (a.norm_w) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
+    else launch_mf<GV_GEGLU, 2, 512, 4, 1, true>(s, a, mf_gu_blocks(), 1, nullptr);  // input already normed
 }
 
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
@@ -665,6 +758,14 @@ int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2
     const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
     launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
     return blocks;
+}
+
+// the K = 16384 down projection of the batched decode step with the next RMSNorm fused into its
+// combine: h (a.out) += down(x); hn = RMSNorm(h) with norm_w (nullptr: h only)
+void gemv_mf_res_norm(hipStream_t s, const GemvArgs& a, float* ws, const uint16_t* norm_w, float eps, uint16_t* hn) {
+    const int KS = a.K / 2048;  // <= 8 (checked by the caller: gemv_res_norm)
+    launch_mf<GV_RES, 1, 512, 4, 2>(s, a, 32, KS, ws);
+    hipLaunchKernelGGL(k_mf_combine_norm, dim3(a.nb), dim3(256), 0, s, ws, KS, a.n_units, a.out, norm_w, eps, hn);
 }
 
 // residual projections; ws: fp32 scratch of KS x nb x N floats for the K split of K = 16384

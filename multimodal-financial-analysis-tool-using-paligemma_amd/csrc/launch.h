@@ -84,6 +84,12 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
 // ws: fp32 scratch (>= 4 x B x N floats) for the MFMA path's K split of K = 16384 (B >= 3)
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
               float* ws);
+// gemv_res, then hn = RMSNorm(h) with norm_w (nullptr: none); on the batched MFMA path the norm is
+// fused into the K-split combine (one workgroup per row)
+void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
+                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn);
+// hn[b] = RMSNorm(x[b]) for nb rows of K (one workgroup per row)
+void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, int nb, int K, uint16_t* out);
 // o_proj + residual whose input is the combine of the decode-attention partials (MQA:
 // n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,

@@ -358,8 +358,38 @@ def _check_tied(lm: "GemmaForCausalLM"):
                                   "call tie_weights() first, as utils.load_hf_model does")
 
 
-def _run_lm(eng, kv_cache, B, L, pos, ids=None, image_feats=None, embeds=None, logits_rows=0):
-    """GemmaModel + lm_head with the cache semantics of KVCache.update (append at num_items())."""
+class _PaddingCheck:
+    """`assert torch.all(attention_mask == 1)` (modeling_gemma.py:558) without a host sync AHEAD of the
+    GPU work: for a device mask the comparison is enqueued first and its result copied to pinned host
+    memory behind an event; wait() reads it -- raising the reference's AssertionError -- after this
+    call's kernels are enqueued and before any Python-side state (the KVCache length) changes, so the
+    GPU never idles while the host waits for the check."""
+
+    _flags = {}
+
+    def __init__(self, mask: torch.Tensor):
+        self.ev, self.bad = None, False
+        if mask.device.type == "cuda":
+            flag = _PaddingCheck._flags.get(mask.device)
+            if flag is None:
+                flag = _PaddingCheck._flags[mask.device] = torch.zeros((), dtype=torch.bool).pin_memory()
+            flag.copy_((mask != 1).any(), non_blocking=True)
+            self.flag = flag
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+        else:
+            self.bad = bool((mask != 1).any())
+
+    def wait(self):
+        if self.ev is not None:
+            self.ev.synchronize()
+            self.bad, self.ev = bool(self.flag), None
+        assert not self.bad, "The input cannot be padded"
+
+
+def _run_lm(eng, kv_cache, B, L, pos, ids=None, image_feats=None, embeds=None, logits_rows=0, before_commit=None):
+    """GemmaModel + lm_head with the cache semantics of KVCache.update (append at num_items());
+    before_commit() runs after the forward is enqueued and before the cache length advances."""
     if kv_cache is None:
         kv = eng.scratch_kv(B, L)
         start = 0
@@ -367,6 +397,8 @@ def _run_lm(eng, kv_cache, B, L, pos, ids=None, image_feats=None, embeds=None, l
         start = kv_cache.num_items()
         kv = kv_cache._ensure(eng, B, start + L)
     logits = eng.lm_forward(kv, start, pos, ids=ids, image_feats=image_feats, embeds=embeds, logits_rows=logits_rows)
+    if before_commit is not None:
+        before_commit()
     if kv_cache is not None:
         kv_cache._len = start + L
     return logits
@@ -473,11 +505,13 @@ class PaliGemmaForConditionalGeneration(nn.Module):
                 attention_mask: Optional[torch.Tensor] = None, inputs_embeds: Optional[torch.FloatTensor] = None,
                 kv_cache: Optional[KVCache] = None, labels: Optional[torch.LongTensor] = None,
                 return_dict: bool = True, **kwargs) -> Tuple:
-        # validation exactly as the reference (modeling_gemma.py:557-564)
+        # validation as the reference (modeling_gemma.py:557-564); the padding check is read after this
+        # call's GPU work is enqueued (_PaddingCheck), still before anything is committed or returned
         if attention_mask is None:
             raise ValueError("attention_mask must be provided")
-        assert torch.all(attention_mask == 1), "The input cannot be padded"
+        chk = _PaddingCheck(attention_mask)
         if inputs_embeds is None and input_ids is None:
+            chk.wait()
             raise ValueError("You must provide either input_ids or inputs_embeds")
         eng = self._pgmi_engine()
         dev = eng.device
@@ -500,6 +534,7 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             merged, mask, position_ids = self._merge_input_ids_with_image_features(
                 image_features=img, inputs_embeds=inputs_embeds.to(dev), input_ids=input_ids.to(dev),
                 attention_mask=attention_mask, kv_cache=kv_cache)
+            chk.wait()
             pos = _merged_positions(position_ids, mask, B, L)
             if kv_cache is not None and cache_len > 0 and L == 1 and bool((pos == pos[0, 0]).all()):
                 # a q_len == 1 step over a filled cache (the ablation harness's decode steps,
@@ -516,7 +551,8 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             # prefill (modeling_gemma.py:532-535: positions 0..L-1), merge on the device
             img = eng.project(eng.vision(pixel_values)) if pixel_values is not None else None
             pos = torch.arange(L).unsqueeze(0).expand(B, L)
-            logits = _run_lm(eng, kv_cache, B, L, pos, ids=input_ids, image_feats=img, logits_rows=rows)
+            logits = _run_lm(eng, kv_cache, B, L, pos, ids=input_ids, image_feats=img, logits_rows=rows,
+                             before_commit=chk.wait)
             if mode == "lazy":
                 logits = LazyLogits(logits, eng.final_hidden(B * L), eng.lm_head, B, L)
         else:
@@ -527,6 +563,7 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             slab = kv_cache._ensure(eng, B, cache_len + 1)
             logits = eng.decode(input_ids, slab, cache_len, position, logits=eng.logits_buffer(B),
                                 graph=self.pgmi_use_graph).clone().unsqueeze(1)
+            chk.wait()
             kv_cache._len = cache_len + 1
 
         loss = None

@@ -144,6 +144,15 @@ int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch
  * the caller's buffer may change between calls. */
 int pgmi_decode_embeds(pgmi_ctx* ctx, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                        int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
+/* pgmi_decode_embeds with the step's inputs left on the device (no host read of a merge's outputs):
+ * position: the merge's (1, 1) position tensor (attention_mask.cumsum(-1)[:, -1:], modeling_gemma.py:526),
+ * dtype PGMI_DTYPE_BF16 / _F32 or 10 = int64, 11 = int32, 12 = float64, rounded to the nearest integer;
+ * mask (may be NULL): the merge's additive mask row over the kv_len + 1 keys (modeling_gemma.py:269),
+ * bf16 (score + mask rounded to bf16) or fp32 (added in fp32, as torch promotes), row stride
+ * mask_b_stride elements.  One sequence (B = 1). */
+int pgmi_decode_embeds_dev(pgmi_ctx* ctx, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                           const void* position, int position_dtype, const void* mask, int mask_dtype,
+                           int64_t mask_b_stride, float* logits, int64_t* next_ids, int use_graph, void* stream);
 /* Prefill graphs (default on): pgmi_vision and pgmi_lm_forward replay a captured hipGraph when
  * called again with identical pointer and size arguments (the graph is captured on the second
  * such call; a replay reads the same addresses as the eager call would).  0 = always eager. */

@@ -63,6 +63,8 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
     short8 qf[8], kf[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) kf[kk] = frag256(krow, kk, lane);
+    // the additive mask of this lane's key (a zero word when there is none): issued with the K rows
+    const float mval = a.mask[(long)b * a.mask_b_stride + (long)(key < Lk ? key : 0) * a.mask_k_stride];
 
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) qf[kk] = frag256(qrow, kk, lane);
@@ -74,8 +76,11 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) acc = mfma16(qf[kk], kf[kk], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? rbf(rbf(acc[r]) * a.scale) : -INFINITY;
+        for (int r = 0; r < 4; ++r) {
+            // bf16(bf16(q.k) * scale), then + mask (:266,269): rounded for a bf16 mask (exact for a zero one)
+            const float sv = rbf(rbf(acc[r]) * a.scale) + mval;
+            S[(lane >> 4) * 4 + r][wave * 16 + (lane & 15)] = kvalid ? (a.mask_round ? rbf(sv) : sv) : -INFINITY;
+        }
     }
     constexpr int VPH = DVH * 32 / 256;  // V chunks per thread per half
     auto stage_v = [&](int half) {      // rows [32 half, 32 half + 32) of the chunk -> Vs
@@ -104,7 +109,8 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int h = wave * 4 + rr;
-            e[rr] = (lane < nk && h < a.G) ? expf(sv[rr] - m[rr]) : 0.f;
+            // (a chunk whose keys are all masked to -inf has m = -inf: e = 0, not exp(NaN))
+            e[rr] = (lane < nk && h < a.G && m[rr] != -INFINITY) ? expf(sv[rr] - m[rr]) : 0.f;
             Ps[h * DPS + lane] = f2bf(e[rr]);
             l[rr] = e[rr];
         }

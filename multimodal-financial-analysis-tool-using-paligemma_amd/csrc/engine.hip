@@ -62,9 +62,10 @@ struct GraphKey {
     int64_t* next;
     const int64_t* ids;  // the ids buffer the graph reads (the context's staging copy, or in place)
     bool emb;            // the step's input is the staged embedding rows (pgmi_decode_embeds), not ids
+    int masked;          // 0: no mask (a zero word), 1: staged bf16 mask (sum rounded), 2: staged fp32 mask
     bool operator<(const GraphKey& o) const {
-        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids, emb) <
-               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids, o.emb);
+        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids, emb, masked) <
+               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids, o.emb, o.masked);
     }
 };
 
@@ -108,6 +109,8 @@ struct pgmi_ctx {
     StepState* pstep;  // the generate-loop prefill's last-row attention (flash-decoding over the prompt's keys)
     int64_t* d_ids;
     uint16_t* d_emb;             // staged input rows of pgmi_decode_embeds ([max_batch][hidden] bf16)
+    float* d_mask;               // staged additive decode mask ([max_batch][max_kv] fp32, pgmi_decode_embeds_dev)
+    float* d_zero;               // one zero word: the "no mask" mask of the decode attention
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
     hipStream_t cap_stream = nullptr;
@@ -596,6 +599,9 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->d_emb, (size_t)B * H))) return rc;
+        if ((rc = dalloc_t(x, &x->d_mask, (size_t)B * c.max_kv))) return rc;
+        if ((rc = dalloc_t(x, &x->d_zero, 64))) return rc;
+        HIPCHK(hipMemset(x->d_zero, 0, 64 * sizeof(float)));
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
@@ -858,6 +864,7 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
                 // would walk every key alone
                 a.Lk = 0;
                 HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x->pstep->kv_len), kv_start + L - 1, 1, s));
+                a.mask = x->d_zero; a.mask_b_stride = 0; a.mask_k_stride = 0; a.mask_round = 1;
                 attention_decode(s, a, x->pstep, kv_start + L, x->opart, x->max_chunks);
                 gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->pstep, TL(x, i, "self_attn.o_proj.weight"), H,
                             x->lastrows, B >= gemv_mf_min_batch() ? x->dAO : nullptr);
@@ -912,7 +919,8 @@ static bool mf_staged() {
 }
 
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
-                       int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr) {
+                       int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr,
+                       int masked = 0) {
     const pgmi_config& c = x->c;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const float eps = c.t_rms_eps;
@@ -943,6 +951,11 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         a.v = Vc; a.v_b_stride = kvb; a.v_row_stride = (int)kvd; a.v_head_stride = HD;
         a.o = x->dAO; a.o_b_stride = (long)H; a.o_row_stride = H; a.o_head_stride = HD;
         a.Lq = 1; a.Lk = 0; a.G = NH / NKV; a.n_kv = NKV; a.B = B; a.scale = 1.0f / std::sqrt((float)HD);
+        if (masked) {  // the staged additive mask (pgmi_decode_embeds_dev), row stride max_kv
+            a.mask = x->d_mask; a.mask_b_stride = c.max_kv; a.mask_k_stride = 1; a.mask_round = masked == 1;
+        } else {
+            a.mask = x->d_zero; a.mask_b_stride = 0; a.mask_k_stride = 0; a.mask_round = 1;
+        }
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
                     B >= gemv_mf_min_batch() ? x->dAO : nullptr);
@@ -974,8 +987,19 @@ int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {
     return 0;
 }
 
+// device-side inputs of a decode step over merged rows (pgmi_decode_embeds_dev): the rotary position
+// and the additive mask come from the caller's merge outputs without a host read
+struct DevStepIn {
+    const void* pos = nullptr;  // (B, 1) position tensor on the device, dtype code (set_step_dev)
+    int pos_dtype = 0;
+    const void* mask = nullptr;  // additive mask rows (kv_len + 1 keys each)
+    int mask_dtype = 0;
+    long mask_b_stride = 0;
+};
+
 static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int B, void* kv, int kv_batch, int kv_max,
-                       int kv_len, int position, float* logits, int64_t* next_ids, int use_graph, void* stream) {
+                       int kv_len, int position, float* logits, int64_t* next_ids, int use_graph, void* stream,
+                       const DevStepIn* dev = nullptr) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;
     const pgmi_config& c = x->c;
@@ -984,12 +1008,22 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
     if ((!ids && !embeds) || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    if (!x->step_known || x->step_kv != kv_len || x->step_pos != position) set_step(s, x->step, kv_len, position);
+    int masked = 0;
+    if (dev) {
+        // position read on the device; the host no longer knows it, so the next call sets the state again
+        set_step_dev(s, x->step, kv_len, dev->pos, dev->pos_dtype);
+        if (dev->mask) {
+            stage_mask(s, dev->mask, dev->mask_dtype, B, dev->mask_b_stride, kv_len + 1, x->d_mask, c.max_kv);
+            masked = dev->mask_dtype == PGMI_DTYPE_F32 ? 2 : 1;
+        }
+    } else if (!x->step_known || x->step_kv != kv_len || x->step_pos != position) {
+        set_step(s, x->step, kv_len, position);
+    }
     // the step advances the device state itself (its last kernel); known only once this call has
     // enqueued its step successfully
     x->step_known = false;
     auto advanced = [&]() {
-        x->step_known = true;
+        x->step_known = dev == nullptr;
         x->step_kv = kv_len + 1;
         x->step_pos = position + 1;
     };
@@ -1000,7 +1034,8 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         erows = x->d_emb;
     }
     if (!use_graph) {
-        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids, erows))) return rc;
+        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids, erows, masked)))
+            return rc;
         LAUNCHCHK();
         advanced();
         return 0;
@@ -1013,11 +1048,12 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         gids = x->d_ids;
     }
     if (embeds) gids = nullptr;
-    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids, embeds != nullptr};
+    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids, embeds != nullptr, masked};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows))) return rc;
+            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked)))
+                return rc;
             LAUNCHCHK();
             advanced();
             return 0;
@@ -1025,7 +1061,7 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows);
+        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
         if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
@@ -1048,6 +1084,23 @@ int pgmi_decode_embeds(pgmi_ctx* x, const void* embeds, int B, void* kv, int kv_
     if (!embeds) return fail(PGMI_E_ARG, "null argument");
     return decode_step(x, nullptr, embeds, B, kv, kv_batch, kv_max, kv_len, position, logits, next_ids, use_graph,
                        stream);
+}
+
+int pgmi_decode_embeds_dev(pgmi_ctx* x, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                           const void* position, int position_dtype, const void* mask, int mask_dtype,
+                           int64_t mask_b_stride, float* logits, int64_t* next_ids, int use_graph, void* stream) {
+    if (!embeds || !position) return fail(PGMI_E_ARG, "null argument");
+    if (position_dtype != PGMI_DTYPE_BF16 && position_dtype != PGMI_DTYPE_F32 && position_dtype != 10 &&
+        position_dtype != 11 && position_dtype != 12)
+        return fail(PGMI_E_ARG, "position dtype must be bf16, fp32, fp64, int64 or int32");
+    if (mask && mask_dtype != PGMI_DTYPE_BF16 && mask_dtype != PGMI_DTYPE_F32)
+        return fail(PGMI_E_ARG, "mask dtype must be bf16 or fp32");
+    if (B != 1) return fail(PGMI_E_ARG, "device-side positions: one sequence per step (B = 1)");
+    DevStepIn d;
+    d.pos = position; d.pos_dtype = position_dtype; d.mask = mask; d.mask_dtype = mask_dtype;
+    d.mask_b_stride = (long)mask_b_stride;
+    return decode_step(x, nullptr, embeds, B, kv, kv_batch, kv_max, kv_len, -1, logits, next_ids, use_graph, stream,
+                       &d);
 }
 
 int pgmi_lm_head(pgmi_ctx* x, const void* normed, int rows, float* logits, void* stream) {

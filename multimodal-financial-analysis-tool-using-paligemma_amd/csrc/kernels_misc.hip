@@ -659,4 +659,36 @@ void set_step(hipStream_t s, StepState* st, int kv_len, int position) {
     hipLaunchKernelGGL(k_set_step, dim3(1), dim3(1), 0, s, st, kv_len, position);
 }
 
+// position = round(pos[0]) (modeling_gemma.py:526's cumsum, float when the mask grew by a float column)
+__global__ void k_set_step_dev(StepState* st, int kv_len, const void* pos, int dtype) {
+    double v;
+    if (dtype == 2) v = (double)*reinterpret_cast<const float*>(pos);
+    else if (dtype == 12) v = *reinterpret_cast<const double*>(pos);
+    else if (dtype == 11) v = (double)*reinterpret_cast<const int32_t*>(pos);
+    else if (dtype == 0) v = (double)bf2f(*reinterpret_cast<const uint16_t*>(pos));
+    else v = (double)*reinterpret_cast<const int64_t*>(pos);
+    st->kv_len = kv_len;
+    st->position = (int)rint(v);
+}
+
+void set_step_dev(hipStream_t s, StepState* st, int kv_len, const void* pos, int dtype) {
+    hipLaunchKernelGGL(k_set_step_dev, dim3(1), dim3(1), 0, s, st, kv_len, pos, dtype);
+}
+
+__global__ void k_stage_mask(const void* src, int dtype, long b_stride, int n, float* dst, int ld) {
+    const int b = blockIdx.y;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const long o = (long)b * b_stride + j;
+        dst[(long)b * ld + j] = dtype == 2 ? reinterpret_cast<const float*>(src)[o]
+                                           : bf2f(reinterpret_cast<const uint16_t*>(src)[o]);
+    }
+}
+
+void stage_mask(hipStream_t s, const void* src, int dtype, int B, long b_stride, int n, float* dst, int ld) {
+    int bx = (n + 255) / 256;
+    if (bx > 64) bx = 64;
+    if (bx < 1) bx = 1;
+    hipLaunchKernelGGL(k_stage_mask, dim3(bx, B), dim3(256), 0, s, src, dtype, b_stride, n, dst, ld);
+}
+
 }  // namespace pgmi

@@ -124,6 +124,13 @@ struct AttnArgs {
     float scale;   // s = bf16(bf16(q.k) * scale)
     float* ws;     // prefill: fp32 scratch for key-split partials (nullptr: no key split)
     long ws_floats;
+    // decode: additive attention mask (modeling_gemma.py:269), fp32, key j of batch row b at
+    // mask[b * mask_b_stride + j * mask_k_stride]; mask_round: the sum is rounded to bf16 (a bf16
+    // mask) or kept in fp32 (an fp32 mask, as torch promotes).  No mask: a zero word with stride 0
+    const float* mask;
+    long mask_b_stride;
+    int mask_k_stride;
+    int mask_round;
 };
 void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
 // decode: Lq == 1, rows = the G heads; keys split over chunks; kv length from StepState (+1)
@@ -184,6 +191,12 @@ void patchify(hipStream_t s, const void* px, int px_is_f32, int B, int C, int H,
               uint16_t* out);
 void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float scale, float offset);
 void set_step(hipStream_t s, StepState* st, int kv_len, int position);
+// step state with the rotary position read on the device: round(pos[0]) of a (B, 1) position tensor
+// of dtype PGMI_DTYPE_* (+ 10 = int64, 11 = int32, 12 = float64) -- no host read of a merge's positions
+void set_step_dev(hipStream_t s, StepState* st, int kv_len, const void* pos, int dtype);
+// an additive mask row set (B rows of n keys, element (b, j) at src[b * b_stride + j], dtype bf16 / fp32)
+// -> fp32 [B][ld]
+void stage_mask(hipStream_t s, const void* src, int dtype, int B, long b_stride, int n, float* dst, int ld);
 // PIL-exact BICUBIC resize of a uint8 HWC RGB image + rescale/normalize -> float32 CHW
 // (processing_paligemma.py:13-49); scratch of preprocess_scratch_bytes() on the device
 size_t preprocess_scratch_bytes(int H, int W, int out_h, int out_w);

@@ -284,6 +284,14 @@ def _positions_2d(position_ids, B, L) -> torch.Tensor:
     return pos.expand(B, L).contiguous()
 
 
+def _dev_mask_ok(mask, n_keys: int) -> bool:
+    """A merge's mask the device-side decode step can take: none, or one additive row over the n_keys
+    attended keys (shape (1, 1, 1, n_keys) as the reference's merge builds it, modeling_gemma.py:512-518)."""
+    if mask is None:
+        return True
+    return torch.is_tensor(mask) and mask.numel() == n_keys and mask.shape[-1] == n_keys and mask.is_floating_point()
+
+
 def _merged_positions(position_ids, mask, B, L) -> torch.Tensor:
     """Host int64 (B, L) positions of a (patched) merge's output, read together with a check of
     its attention mask in ONE device->host copy.  libpgmi attends every cached key with no
@@ -534,6 +542,18 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             merged, mask, position_ids = self._merge_input_ids_with_image_features(
                 image_features=img, inputs_embeds=inputs_embeds.to(dev), input_ids=input_ids.to(dev),
                 attention_mask=attention_mask, kv_cache=kv_cache)
+            if (kv_cache is not None and cache_len > 0 and L == 1 and B == 1 and torch.is_tensor(position_ids)
+                    and position_ids.numel() == 1 and _dev_mask_ok(mask, cache_len + 1)):
+                # a one-sequence q_len == 1 step over a filled cache (the ablation harness's decode steps,
+                # ablation_study_fixed.py:215-221,239-243): the graphed decode step reads the merge's
+                # position and additive mask on the device -- no host read before the step is enqueued
+                slab = kv_cache._ensure(eng, B, cache_len + 1)
+                logits = eng.decode_embeds_dev(merged[:, 0], slab, cache_len, position_ids,
+                                               mask if torch.is_tensor(mask) else None, logits=eng.logits_buffer(B),
+                                               graph=self.pgmi_use_graph).clone().unsqueeze(1)
+                chk.wait()
+                kv_cache._len = cache_len + 1
+                return self._pack(logits, labels, kv_cache, return_dict)
             chk.wait()
             pos = _merged_positions(position_ids, mask, B, L)
             if kv_cache is not None and cache_len > 0 and L == 1 and bool((pos == pos[0, 0]).all()):
@@ -566,6 +586,10 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             chk.wait()
             kv_cache._len = cache_len + 1
 
+        return self._pack(logits, labels, kv_cache, return_dict)
+
+    def _pack(self, logits, labels, kv_cache, return_dict):
+        """The loss and return conventions of modeling_gemma.py:598-617."""
         loss = None
         if labels is not None:
             shift_logits = logits[..., :-1, :].contiguous()

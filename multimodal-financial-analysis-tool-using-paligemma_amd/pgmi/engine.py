@@ -301,6 +301,39 @@ class Engine:
                 "pgmi_decode_embeds")
         return logits
 
+    _POS_DTYPES = {torch.bfloat16: 0, torch.float32: 2, torch.int64: 10, torch.int32: 11, torch.float64: 12}
+
+    def decode_embeds_dev(self, embeds: torch.Tensor, kv: torch.Tensor, kv_len: int, position: torch.Tensor,
+                          mask: torch.Tensor = None, logits: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
+        """decode_embeds for one sequence with its rotary position and additive mask left on the device
+        (a merge's outputs, read by the step itself: no host sync).  position: one element; mask:
+        kv_len + 1 additive values (bf16 or fp32; other float dtypes are promoted to fp32)."""
+        self._ready()
+        e = embeds.to(self.device, torch.bfloat16).reshape(-1, self.cfgd["t_hidden"]).contiguous()
+        if e.shape[0] != 1:
+            raise ValueError("decode_embeds_dev: one sequence per step")
+        p = position.to(self.device).reshape(-1)[:1]
+        if p.dtype not in self._POS_DTYPES:
+            p = p.to(torch.float64)
+        p = p.contiguous()
+        mp, mdt = None, N.DTYPE_BF16
+        if mask is not None:
+            m = mask.to(self.device).reshape(-1)
+            if m.numel() != kv_len + 1:
+                raise ValueError(f"mask has {m.numel()} keys, the step attends {kv_len + 1}")
+            if m.dtype not in (torch.bfloat16, torch.float32):
+                m = m.float()
+            mp = m.contiguous()
+            mdt = N.DTYPE_F32 if mp.dtype == torch.float32 else N.DTYPE_BF16
+        if logits is None:
+            logits = torch.empty((1, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        N.check(self.lib.pgmi_decode_embeds_dev(self.ctx, e.data_ptr(), 1, kv.data_ptr(), kv.shape[2], kv.shape[3],
+                                                kv_len, p.data_ptr(), self._POS_DTYPES[p.dtype], N.ptr(mp), mdt,
+                                                mp.numel() if mp is not None else 0, logits.data_ptr(), None,
+                                                int(graph), self._s()),
+                "pgmi_decode_embeds_dev")
+        return logits
+
     def set_prefill_graph(self, on: bool) -> None:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")

@@ -259,9 +259,10 @@ def gemma_mlp(P, i, x):
     return linear(bf16(g * u), P[pre + "down_proj.weight"])
 
 
-def gemma_forward(P, cfg, embeds, positions, kv, invf=None, taps=None, all_logits=True):
+def gemma_forward(P, cfg, embeds, positions, kv, invf=None, taps=None, all_logits=True, mask=None):
     """GemmaForCausalLM.forward (modeling_gemma.py:399-427) over GemmaModel.forward
-    (:357-382) and GemmaDecoderLayer.forward (:307-338)."""
+    (:357-382) and GemmaDecoderLayer.forward (:307-338); mask: the additive attention mask every
+    layer adds (:269), None = the merge's zero mask."""
     t = cfg["text_config"]
     eps = t.get("rms_norm_eps", 1e-6)
     if invf is None:
@@ -271,7 +272,7 @@ def gemma_forward(P, cfg, embeds, positions, kv, invf=None, taps=None, all_logit
     for i in range(t["num_hidden_layers"]):
         pre = f"language_model.model.layers.{i}."
         x = rms_norm(h, P[pre + "input_layernorm.weight"], eps)
-        x = gemma_attention(P, cfg, i, x, positions, kv, invf)
+        x = gemma_attention(P, cfg, i, x, positions, kv, invf, mask=mask)
         h = bf16(x + h)
         x = rms_norm(h, P[pre + "post_attention_layernorm.weight"], eps)
         x = gemma_mlp(P, i, x)

@@ -391,3 +391,41 @@ def test_rccl_weight_broadcast_single_rank(eng):
         N.check(lib.pgmi_comm_destroy(comm))
     assert torch.equal(eng.slab[::4099], before)
     eng.prepare()
+
+
+@pytest.mark.parametrize("mask_dtype", ["bf16", "fp32"])
+def test_decode_embeds_dev_position_and_mask(eng, gold, mask_dtype):
+    """pgmi_decode_embeds_dev (the ablation harness's q_len == 1 steps without a host read): the
+    rotary position and the additive mask are read on the device.  A zero mask gives exactly the
+    host-position step's logits; a mask hiding the first 40 keys matches the oracle with the same
+    additive mask (modeling_gemma.py:269; bf16 mask: score + mask rounded to bf16, fp32 mask: added
+    in fp32)."""
+    cfg = W.small_config()
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    L = ids.shape[1]
+    feats = eng.project(eng.vision(px))
+    kv = eng.new_kv(1, 1024)
+    eng.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)
+    tok = 108
+    row = eng.embed(torch.tensor([[tok]], device="cuda"))[:, 0]
+    host = eng.decode_embeds(row, kv, L, L + 1, graph=False).clone()
+    dt = torch.bfloat16 if mask_dtype == "bf16" else torch.float32
+    pos = torch.tensor([[float(L + 1)]], device="cuda")
+    zero = torch.zeros((1, 1, 1, L + 1), dtype=dt, device="cuda")
+    dev = eng.decode_embeds_dev(row, kv, L, pos, zero, graph=False).clone()
+    assert torch.equal(host, dev)
+    m = torch.zeros((1, 1, 1, L + 1), dtype=torch.float32)
+    m[..., :40] = -1e4
+    got = eng.decode_embeds_dev(row, kv, L, pos, m.to("cuda", dt), graph=False).clone().cpu().numpy()[0]
+    # the oracle over the same prompt, then the one-token step with the same additive mask
+    P = W.synthetic_state_dict_f32(cfg, SEED)
+    _, okv = O.paligemma_prefill(P, cfg, gold["ids"], O.from_bits(gold["pixels_bits"]), all_logits=False)
+    emb = O.merge(P, cfg, None, np.array([[tok]]))
+    # (unmasked keys add an exact 0 in either dtype; masked ones vanish from the softmax in both, so the
+    # oracle's bf16 add is the reference for both mask dtypes)
+    ref = O.gemma_forward(P, cfg, emb, np.full((1, 1), L + 1), okv, mask=O.bf16(m.numpy()))[0, -1]
+    assert rel_l2(got, ref) < 3e-2, rel_l2(got, ref)
+    top = np.argsort(ref)[-8:]
+    assert np.abs(got[top] - ref[top]).max() <= 0.25
+    assert rel_l2(got, host.cpu().numpy()[0]) > 1e-3  # the mask changed the step

@@ -113,6 +113,7 @@ struct pgmi_ctx {
     float* d_zero;               // one zero word: the "no mask" mask of the decode attention
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
+    unsigned* arrive;            // per decode layer: chunk counter of the fused attention + o_proj launch
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
@@ -603,6 +604,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->d_zero, 64))) return rc;
         HIPCHK(hipMemset(x->d_zero, 0, 64 * sizeof(float)));
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
+        if ((rc = dalloc_t(x, &x->arrive, (size_t)(c.t_layers > 0 ? c.t_layers : 1) * 32))) return rc;  // 128 B each
+        HIPCHK(hipMemset(x->arrive, 0, (size_t)(c.t_layers > 0 ? c.t_layers : 1) * 32 * sizeof(unsigned)));
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
@@ -942,9 +945,11 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+        const bool fused = NKV == 1 && attn_ores_fused(B);  // attention + o_proj as one launch (B <= 2)
+        unsigned* arrive = fused ? x->arrive + (size_t)i * 32 : nullptr;
         gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
                  TL(x, i, "self_attn.q_proj.weight"), x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws,
-                 (fold && i == 0) ? &emb : nullptr);
+                 (fold && i == 0) ? &emb : nullptr, arrive);
         AttnArgs a{};
         a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -956,9 +961,14 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         } else {
             a.mask = x->d_zero; a.mask_b_stride = 0; a.mask_k_stride = 0; a.mask_round = 1;
         }
-        attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
-        gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                    B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+        if (fused) {
+            attn_ores(s, B, a, x->step, launch_keys, x->opart, x->max_chunks, TL(x, i, "self_attn.o_proj.weight"), H,
+                      x->dH, arrive);
+        } else {
+            attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
+            gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
+                        B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+        }
         if (mf) {
             rows_norm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, B, H, x->dHn);
             gemv_geglu(s, B, x->dHn, nullptr, eps, TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);

@@ -105,19 +105,20 @@ def test_ablation_kv_mode_teacher_forced(model, G):
     px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
     eng = model._pgmi_engine()
     calls = []
-    orig = eng.decode_embeds
+    orig = eng.decode_embeds_dev
 
     def counting(*a, **k):
         calls.append(1)
         return orig(*a, **k)
 
-    eng.decode_embeds = counting
+    eng.decode_embeds_dev = counting
     try:
         n = len(g["kv_tokens"])
         logits, picks, pre = run_harness(model, ids, px, True, n, teacher=g["kv_tokens"])
     finally:
-        del eng.decode_embeds
-    # every q_len == 1 step took the graphed decode step over the merged row
+        del eng.decode_embeds_dev
+    # every q_len == 1 step took the graphed decode step over the merged row, with the merge's position
+    # and mask read on the device (pgmi_decode_embeds_dev: no host read per step)
     assert len(calls) == n - 1
     top = torch.gather(pre[0], 0, torch.from_numpy(g["kv_prefill_topk_idx"][0]).cuda()).cpu().numpy()
     assert np.abs(top - g["kv_prefill_topk_val"][0]).max() <= 0.25

@@ -144,3 +144,16 @@ def remove_ablation_patches(model):
     model.__dict__.pop("_merge_input_ids_with_image_features", None)
     for layer in model.language_model.model.layers:
         layer.self_attn.rotary_emb.__dict__.pop("forward", None)
+
+
+def assert_within_floor(label, got, ref_bf16, ref_fp32, base=1e-2, factor=STEP_FLOOR_FACTOR):
+    """Module-level form of the floor rule: rel-L2 of our output vs the oracle bf16
+    <= max(base, factor x the oracle bf16's own rel-L2 vs its fp32 truth) -- for module chains whose
+    bf16 rounding noise alone approaches the kernel-level 1e-2 bound (a Gemma attention: 0.96e-2, a
+    whole decoder layer + final norm: 1.22e-2 on the module tests' inputs)."""
+    r = rel_l2(got, ref_bf16)
+    floor = rel_l2(ref_bf16, ref_fp32)
+    bound = max(base, factor * floor)
+    print("module-parity " + json.dumps({"label": label, "rel_vs_oracle_bf16": r, "oracle_bf16_vs_fp32": floor,
+                                           "bound": bound}))
+    assert r <= bound, (label, r, bound, floor)

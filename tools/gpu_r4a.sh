@@ -8,7 +8,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out
 mkdir -p $O
 export PGMI_PARITY_LOG=$O/parity_tests.jsonl
-T=${1:-"tests/test_gpu_modules.py tests/test_gpu_api.py tests/test_gpu_model_small.py tests/test_gpu_full.py tests/test_gpu_full_batch.py"}
+T=${1:-"tests/test_gpu_modules.py tests/test_gpu_api.py tests/test_gpu_model_small.py tests/test_gpu_ablation.py tests/test_gpu_full.py tests/test_gpu_full_batch.py"}
 cd $R
 timeout -k 10 900 python -u -m pytest $T -x -v --timeout 300 --timeout-method thread > $O/t1.log 2>&1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
@@ -18,5 +18,13 @@ for i in 1 2; do
     PGMI_MF_STAGED=$v timeout -k 10 300 python bench.py --batch 8 --steps 64 --warmup 8 --no-448 --no-extra --no-api \
       --no-cpu-baseline --prefill-iters 3 > $O/b8.log 2>&1
     echo "staged=$v $(tail -n 1 $O/b8.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["prefill_ms"])')" >> $O/b8ab.txt
+  done
+done
+# same-box A/B of the B = 1 step: fused attention + o_proj launch (default) vs the two launches
+for i in 1 2; do
+  for v in 0 1; do
+    PGMI_FUSED_ATTN=$v timeout -k 10 300 python bench.py --steps 256 --warmup 16 --no-448 --no-extra --no-api \
+      --no-cpu-baseline --prefill-iters 3 > $O/b1.log 2>&1
+    echo "fused=$v $(tail -n 1 $O/b1.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["prefill_ms"])')" >> $O/b1ab.txt
   done
 done

@@ -207,6 +207,13 @@ int pgmi_preprocess(pgmi_ctx* ctx, const void* src_hwc, int H, int W, int out_h,
  * (modeling_gemma.py:134), 1 = down projection (split-K partials, as the prefill runs it). */
 int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* stream);
 
+/* In-situ timing probe of the prefill MLP GEMMs (measurement only): on != 0 makes every following
+ * pgmi_lm_forward eager (prefill graphs off) and brackets each layer's gate|up + GeGLU GEMM and down
+ * GEMM (modeling_gemma.py:133-134) with HIP events; pgmi_prefill_probe_times writes the last probed
+ * forward's durations in microseconds: us[i] = layer i's gate|up, us[layers + i] = its down.  on = 0
+ * restores the graphs. */
+int pgmi_prefill_probe(pgmi_ctx* ctx, int on);
+int pgmi_prefill_probe_times(pgmi_ctx* ctx, float* us, int n);
 /* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent
  * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles, 30-35 warp-specialised panel tiles);
  * cfg < 0 restores the automatic (measured) plan. */

@@ -31,13 +31,12 @@ __device__ __forceinline__ short8 frag256(const uint16_t* rowp, int kk, int lane
     return __builtin_bit_cast(short8, ldg16(rowp + k));
 }
 
-// COH (the fused attention + o_proj launch, kernels_fused.hip): the partial record is published
-// write-through and the chunk's arrival counted on `arrive` once every store has drained, so
-// o_proj workgroups of the same launch read it coherently after the count completes
+// COH (the batched attention + combine launch, kernels_fused.hip): the partial record is published
+// write-through and every lane's stores have drained when the block returns (after a barrier), so the
+// caller may count the chunk's arrival and another workgroup of the launch read the record coherently
 template <bool COH = false>
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
-                                                  int max_chunks, int chunk, int kvh, int b, unsigned char* lds,
-                                                  unsigned* arrive = nullptr) {
+                                                  int max_chunks, int chunk, int kvh, int b, unsigned char* lds) {
     const int kv_len = st->kv_len;
     const int Lk = kv_len + 1;
     const int nch = (Lk + DCH - 1) / DCH;
@@ -172,11 +171,9 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
         }
     }
     if (tid < 32) stxf<COH>(pb + 16 * 256 + tid, stat[tid >> 4][tid & 15]);
-    if constexpr (COH) {
-        // coh.h protocol: every lane drains its write-through stores, then one count per chunk
+    if constexpr (COH) {  // coh.h protocol: every lane drains its write-through stores before the count
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -113,7 +113,7 @@ struct pgmi_ctx {
     float* d_zero;               // one zero word: the "no mask" mask of the decode attention
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
-    unsigned* arrive;            // per decode layer: chunk counter of the fused attention + o_proj launch
+    unsigned* arrive_rows;       // per batch row: chunk counter of the batched attention + combine launch
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
@@ -124,6 +124,10 @@ struct pgmi_ctx {
     bool step_known = false;
     int step_kv = 0, step_pos = 0;
     std::map<std::vector<intptr_t>, GraphEntry> pgraphs;
+    // in-situ timing probe of the prefill MLP GEMMs (pgmi_prefill_probe): events around layer i's gate|up
+    // GEMM (ev[4i], ev[4i+1]) and down GEMM (ev[4i+2], ev[4i+3]) of eager forwards
+    std::vector<hipEvent_t> probe_ev;
+    bool probe_on = false;
 };
 
 namespace {
@@ -346,6 +350,8 @@ int pgmi_create(int device, const pgmi_config* cfg, pgmi_ctx** out) {
 }
 
 int pgmi_destroy(pgmi_ctx* x) {
+    if (x)
+        for (auto& e : x->probe_ev) (void)hipEventDestroy(e);
     if (!x) return 0;
     for (auto& kv : x->graphs)
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
@@ -604,8 +610,8 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->d_zero, 64))) return rc;
         HIPCHK(hipMemset(x->d_zero, 0, 64 * sizeof(float)));
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
-        if ((rc = dalloc_t(x, &x->arrive, (size_t)(c.t_layers > 0 ? c.t_layers : 1) * 32))) return rc;  // 128 B each
-        HIPCHK(hipMemset(x->arrive, 0, (size_t)(c.t_layers > 0 ? c.t_layers : 1) * 32 * sizeof(unsigned)));
+        if ((rc = dalloc_t(x, &x->arrive_rows, (size_t)B * 32))) return rc;
+        HIPCHK(hipMemset(x->arrive_rows, 0, (size_t)B * 32 * sizeof(unsigned)));
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
@@ -889,12 +895,17 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
                         R, H);
         EpiArgs g{};
         g.out = x->ACT; g.ldo = c.t_intermediate;
+        const bool probe = x->probe_on && (size_t)(4 * i + 3) < x->probe_ev.size();
+        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i], s));
         gemm(s, x->Tn, H, TL(x, i, "mlp.gate_proj.weight"), H, R, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
              x->ws_bytes, c.t_intermediate);
+        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 1], s));
         EpiArgs d{};
         d.res = x->Hs; d.ldr = H; d.out = x->Hs; d.ldo = H;
+        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 2], s));
         sp = gemm(s, x->ACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, R, H,
                   c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes, 0, true);
+        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 3], s));
         const bool last = i + 1 == c.t_layers;
         splitk_res_norm(s, x->ws, sp, nullptr, x->Hs, last ? fnorm : TL(x, i + 1, "input_layernorm.weight"), nullptr,
                         eps, x->Tn, R, H);
@@ -914,10 +925,11 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
-// probe knob: PGMI_MF_STAGED=1 keeps the round-3 batched form (each projection stages and normalises its
-// rows itself) for same-box A/Bs
+// The batched form's RMSNorms: staged by each projection itself (default) or computed once per row
+// (k_rows_norm / the combine's fused norm) and read unstaged -- measured equal (B = 8 step 1.5449 vs
+// 1.5452 ms, same box), so the form with fewer launches stays; PGMI_MF_STAGED=0 selects the other
 static bool mf_staged() {
-    static const bool v = [] { const char* e = getenv("PGMI_MF_STAGED"); return e && atoi(e) != 0; }();
+    static const bool v = [] { const char* e = getenv("PGMI_MF_STAGED"); return !e || atoi(e) != 0; }();
     return v;
 }
 
@@ -945,11 +957,9 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
-        const bool fused = NKV == 1 && attn_ores_fused(B);  // attention + o_proj as one launch (B <= 2)
-        unsigned* arrive = fused ? x->arrive + (size_t)i * 32 : nullptr;
         gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
                  TL(x, i, "self_attn.q_proj.weight"), x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws,
-                 (fold && i == 0) ? &emb : nullptr, arrive);
+                 (fold && i == 0) ? &emb : nullptr);
         AttnArgs a{};
         a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -961,9 +971,11 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         } else {
             a.mask = x->d_zero; a.mask_b_stride = 0; a.mask_k_stride = 0; a.mask_round = 1;
         }
-        if (fused) {
-            attn_ores(s, B, a, x->step, launch_keys, x->opart, x->max_chunks, TL(x, i, "self_attn.o_proj.weight"), H,
-                      x->dH, arrive);
+        if (B >= gemv_mf_min_batch() && NKV == 1 && attn_comb_fused(B)) {
+            // the combine runs in the attention launch (its last chunk per row), o_proj reads dAO
+            attention_decode_comb(s, a, x->step, launch_keys, x->opart, x->max_chunks, x->arrive_rows);
+            gemv_o_attn(s, B, NH, nullptr, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
+                        x->dAO);
         } else {
             attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
             gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
@@ -987,6 +999,34 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
                      x->pidx, &nparts, x->lm_done, nx, x->step))
         argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
+    return 0;
+}
+
+int pgmi_prefill_probe(pgmi_ctx* x, int on) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    if (on && x->probe_ev.empty()) {
+        x->probe_ev.resize((size_t)4 * x->c.t_layers);
+        for (auto& e : x->probe_ev) HIPCHK(hipEventCreate(&e));
+    }
+    x->probe_on = on != 0;
+    x->prefill_graph = !x->probe_on;  // the probe records its events in eager forwards
+    clear_pgraphs(x);
+    return 0;
+}
+
+int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
+    if (!x || !us) return fail(PGMI_E_ARG, "null argument");
+    if (x->probe_ev.empty()) return fail(PGMI_E_STATE, "pgmi_prefill_probe(ctx, 1) has not been called");
+    const int L = x->c.t_layers;
+    if (n < 2 * L) return fail(PGMI_E_ARG, "us needs 2 x layers entries");
+    HIPCHK(hipEventSynchronize(x->probe_ev.back()));
+    for (int i = 0; i < L; ++i) {
+        float a = 0.f, b = 0.f;
+        HIPCHK(hipEventElapsedTime(&a, x->probe_ev[4 * i], x->probe_ev[4 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&b, x->probe_ev[4 * i + 2], x->probe_ev[4 * i + 3]));
+        us[i] = a * 1e3f;
+        us[L + i] = b * 1e3f;
+    }
     return 0;
 }
 

@@ -66,11 +66,6 @@ struct GemvArgs {
     float normalizer;
     int64_t pad_id;
     uint16_t* emb_out;
-    // ORES inside the fused attention + o_proj launch (kernels_fused.hip): the chunk arrival counter
-    // the prologue waits on (nch x nb arrivals) before it reads the partials coherently; QKV: the
-    // counter this layer's fused launch will count on, zeroed by workgroup 0 (the launches are
-    // stream-ordered, so the fused launch starts from 0)
-    unsigned* arrive;
 };
 
 // WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their
@@ -78,7 +73,7 @@ struct GemvArgs {
 // XREG: the activation lives in registers (lane's own K chunks), the RMSNorm is computed
 // per wave (WK == 1: every wave holds the whole row), no LDS staging / barrier; used when
 // B * K/(512*WK) chunks fit in 32 VGPRs.  Otherwise the activation is staged in LDS.
-template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH = 1, bool EMB = false, bool FUSED = false>
+template <int B, int KCH, int RPW, int MODE, int WK, bool XREG, int DEPTH = 1, bool EMB = false>
 __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, const int nblk, uint16_t* xs) {
     static_assert(!EMB || (MODE == GV_QKV && XREG && WK == 1), "embedding fold: register-held q|k|v input only");
     constexpr int NR = (MODE == GV_QKV || MODE == GV_GEGLU) ? 2 : 1;
@@ -178,24 +173,6 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
         const int nch = (a.st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
         constexpr int CMAX = 12;  // chunks held in registers (768 keys); longer caches take two passes
         const int nitems = a.nb * K / 8;
-        // fused launch: wait (one lane, with s_sleep) until every chunk of every row has published its
-        // partial record; bounded -- on a give-up the output is poisoned (NaN), never a hang
-        bool poison = false;
-        if constexpr (FUSED) {
-            __shared__ int gave_up;
-            if (tid == 0) {
-                const unsigned target = (unsigned)(nch * a.nb);
-                unsigned it = 0;
-                int g = 0;
-                while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++it > (1u << 24)) { g = 1; break; }
-                }
-                gave_up = g;
-            }
-            __syncthreads();
-            poison = gave_up != 0;
-        }
         for (int e8 = tid; e8 < nitems; e8 += 256) {
             const int b = e8 / (K / 8), e = (e8 % (K / 8)) * 8;
             const int h = e >> 8;
@@ -213,10 +190,10 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 #pragma unroll
                 for (int c = 0; c < CMAX; ++c) {
                     const long cs = (long)(c < nch ? c : nch - 1) * kAttnPartStride;
-                    x0[c] = ldxf4<FUSED>(pb + cs);
-                    x1[c] = ldxf4<FUSED>(pb + cs + 4);
-                    mc[c] = ldxf<FUSED>(sp + cs);
-                    lc[c] = ldxf<FUSED>(sp + cs + 16);
+                    x0[c] = ldxf4<false>(pb + cs);
+                    x1[c] = ldxf4<false>(pb + cs + 4);
+                    mc[c] = ldxf<false>(sp + cs);
+                    lc[c] = ldxf<false>(sp + cs + 16);
                 }
 #pragma unroll
                 for (int c = 0; c < CMAX; ++c)
@@ -230,19 +207,19 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                         for (int j = 0; j < 4; ++j) { o[j] += w * x0[c][j]; o[4 + j] += w * x1[c][j]; }
                     }
             } else {
-                for (int c = 0; c < nch; ++c) M = fmaxf(M, ldxf<FUSED>(sp + (long)c * kAttnPartStride));
+                for (int c = 0; c < nch; ++c) M = fmaxf(M, ldxf<false>(sp + (long)c * kAttnPartStride));
                 for (int c = 0; c < nch; ++c) {
-                    const float w = expf(ldxf<FUSED>(sp + (long)c * kAttnPartStride) - M);
-                    S += w * ldxf<FUSED>(sp + (long)c * kAttnPartStride + 16);
-                    const f32x4 x0 = ldxf4<FUSED>(pb + (long)c * kAttnPartStride);
-                    const f32x4 x1 = ldxf4<FUSED>(pb + (long)c * kAttnPartStride + 4);
+                    const float w = expf(ldxf<false>(sp + (long)c * kAttnPartStride) - M);
+                    S += w * ldxf<false>(sp + (long)c * kAttnPartStride + 16);
+                    const f32x4 x0 = ldxf4<false>(pb + (long)c * kAttnPartStride);
+                    const f32x4 x1 = ldxf4<false>(pb + (long)c * kAttnPartStride + 4);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) { o[j] += w * x0[j]; o[4 + j] += w * x1[j]; }
                 }
             }
             u16x8 ob;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ob.v[j] = poison ? (uint16_t)0x7FC0 : f2bf(o[j] / S);
+            for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(o[j] / S);
             *reinterpret_cast<u16x8*>(xs + b * K + e) = ob;
             if (a.o_out && blk == 0) *reinterpret_cast<u16x8*>(a.o_out + (long)b * K + e) = ob;
         }
@@ -342,7 +319,6 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
 
     int kv_len = 0, pos = 0;
     if constexpr (MODE == GV_QKV) {
-        if (a.arrive && blk == 0 && tid == 0) __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         kv_len = a.st->kv_len;
         pos = a.st->position;
         if (pos < 0) pos = 0;

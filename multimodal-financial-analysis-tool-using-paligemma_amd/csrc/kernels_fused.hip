@@ -1,16 +1,8 @@
-// kernels_fused.hip -- the decode step's attention and o_proj as ONE launch (B <= 2, the v_dot2 path).
+// kernels_fused.hip -- decode attention with its flash-decoding combine in the same launch (B >= 3).
 //
-// Separately, GemmaAttention's flash-decoding chunks (k_attn_decode, 5-9 workgroups) and the o_proj
-// GEMV with the chunk combine in its prologue (gemv_body.h GV_ORES, 256 workgroups) are two
-// latency-bound launches (≈5.9 + 5.3 µs, 8 MB of weights between them).  Here the chunk workgroups
-// come first in the grid and the o_proj workgroups after them:
-//   - a chunk workgroup runs attn_decode_block, publishes its partial record write-through and counts
-//     its arrival on the layer's counter once its stores have drained (coh.h protocol);
-//   - an o_proj workgroup issues its weight stream first, then waits (one lane, s_sleep, bounded) for
-//     nch x B arrivals, reads the records coherently, combines and multiplies.
-// The chunk workgroups never wait and have the lowest workgroup ids, so they are dispatched before
-// any o_proj workgroup on every XCD: no residency assumption, no deadlock.  The counter is zeroed by
-// the layer's q|k|v launch (stream-ordered before this one).  The arithmetic is the two-launch form's.
+// (Round 4 also built and measured the B <= 2 attention + o_proj as one launch -- chunk workgroups
+// publishing write-through and counting, o_proj workgroups of the same grid waiting on the count: B = 1
+// step 1.059 -> 1.121 ms, slower than the two launches, and removed)
 #include <cstdlib>
 
 #include "attn_decode_body.h"
@@ -18,39 +10,63 @@
 
 namespace pgmi {
 
-template <int B>
-__global__ void __launch_bounds__(256) k_attn_ores(AttnArgs a, GemvArgs g, float* __restrict__ part, int max_chunks,
-                                                   int nchg) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // o_proj: the combined rows [B][K]
-    __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
-    const int n_attn = nchg * B;
-    const int bx = blockIdx.x;
-    if (bx < n_attn) {
-        attn_decode_block<true>(a, g.st, part, max_chunks, bx % nchg, 0, bx / nchg, lds, g.arrive);
-        return;
+// ---------------------------------------------------------------- B >= 3: attention + its combine
+// Flash-decoding chunks as k_attn_decode, each publishing its record write-through and counting on its
+// row's counter; the chunk that arrives last for row b combines the row's records (coherent loads, the
+// fixed chunk order of k_attn_combine) and writes o[b] -- the k_attn_combine launch disappears, no
+// workgroup waits.  The last arriver re-arms the counter for the next step.
+__device__ __forceinline__ void attn_combine_row(const float* __restrict__ part, int max_chunks, int nch, int b,
+                                                 int K, uint16_t* __restrict__ o) {
+    for (int e8 = threadIdx.x; e8 < K / 8; e8 += blockDim.x) {
+        const int e = e8 * 8, h = e >> 8;
+        const float* pb = part + (long)b * max_chunks * kAttnPartStride + h * 256 + (e & 255);
+        const float* sp = part + (long)b * max_chunks * kAttnPartStride + 16 * 256 + h;
+        float M = -INFINITY, S = 0.f, acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+        for (int c = 0; c < nch; ++c) M = fmaxf(M, ldf_coh(sp + (long)c * kAttnPartStride));
+        for (int c = 0; c < nch; ++c) {
+            const float w = expf(ldf_coh(sp + (long)c * kAttnPartStride) - M);
+            S += w * ldf_coh(sp + (long)c * kAttnPartStride + 16);
+            const f32x4 x0 = __builtin_bit_cast(f32x4, ld16_coh(pb + (long)c * kAttnPartStride));
+            const f32x4 x1 = __builtin_bit_cast(f32x4, ld16_coh(pb + (long)c * kAttnPartStride + 4));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { acc[j] += w * x0[j]; acc[4 + j] += w * x1[j]; }
+        }
+        u16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ob.v[j] = f2bf(acc[j] / S);
+        *reinterpret_cast<u16x8*>(o + (long)b * K + e) = ob;
     }
-    gemv_block<B, 4, 2, GV_ORES, 1, false, 1, false, true>(g, bx - n_attn, (int)gridDim.x - n_attn, xs);
 }
 
-bool attn_ores_fused(int B) {
-    static const bool off = [] { const char* e = getenv("PGMI_FUSED_ATTN"); return e && atoi(e) == 0; }();
-    return !off && B <= 2;
+__global__ void __launch_bounds__(256) k_attn_decode_comb(AttnArgs a, const StepState* st, float* __restrict__ part,
+                                                          int max_chunks, unsigned* __restrict__ cnt) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kAttnDecodeLds];
+    __shared__ int last;
+    const int b = blockIdx.z;
+    const int nch = (st->kv_len + 1 + kAttnChunk - 1) / kAttnChunk;
+    if ((int)blockIdx.x >= nch) return;  // (attn_decode_block returns there too, before counting)
+    unsigned* c = cnt + (long)b * 32;
+    attn_decode_block<true>(a, st, part, max_chunks, blockIdx.x, blockIdx.y, b, lds);
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)nch;
+    __syncthreads();
+    if (!last) return;
+    attn_combine_row(part, max_chunks, nch, b, a.G * 256, a.o + (long)b * a.o_b_stride);
+    if (threadIdx.x == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-void attn_ores(hipStream_t s, int B, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
-               int max_chunks, const uint16_t* Wo, int N, uint16_t* h_inout, unsigned* arrive) {
+bool attn_comb_fused(int B) {
+    static const bool off = [] { const char* e = getenv("PGMI_FUSED_COMB"); return e && atoi(e) == 0; }();
+    return !off && B >= 3;
+}
+
+void attention_decode_comb(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
+                           int max_chunks, unsigned* cnt) {
     int nch = (launch_keys + kAttnChunk - 1) / kAttnChunk;
     if (nch > max_chunks) nch = max_chunks;
-    GemvArgs g{};
-    g.x = nullptr; g.norm_w = nullptr; g.W = Wo; g.n_units = N; g.K = a.G * 256; g.nb = B; g.out = h_inout;
-    g.part = part; g.max_chunks = max_chunks; g.G = a.G; g.st = st; g.o_out = nullptr; g.arrive = arrive;
-    constexpr int per_block = 4 * 2;  // 4 unit groups x 2 rows (the two-launch form's o_proj grid)
-    const int oblocks = (N + per_block - 1) / per_block;
-    const size_t lds = (size_t)B * g.K * sizeof(uint16_t);
-    if (B <= 1)
-        hipLaunchKernelGGL(k_attn_ores<1>, dim3(nch * 1 + oblocks), dim3(256), lds, s, a, g, part, max_chunks, nch);
-    else
-        hipLaunchKernelGGL(k_attn_ores<2>, dim3(nch * 2 + oblocks), dim3(256), lds, s, a, g, part, max_chunks, nch);
+    hipLaunchKernelGGL(k_attn_decode_comb, dim3(nch, a.n_kv, a.B), dim3(256), 0, s, a, st, part, max_chunks, cnt);
 }
 
 }  // namespace pgmi

@@ -33,10 +33,8 @@ bool gemv_qkv_folds_embed(int B) { return B <= 2 && B < gemv_mf_min_batch(); }
 
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
-              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws, const EmbedFold* emb,
-              unsigned* arrive) {
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws, const EmbedFold* emb) {
     GemvArgs a{};
-    a.arrive = arrive;
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wqkv; a.n_units = (nh + 2 * nkv) * 128; a.K = 2048; a.nb = B;
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
     a.kv_b_stride = kv_b_stride; a.nkv = nkv;

@@ -743,7 +743,8 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     const int K = a.K;
-    hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 63) / 64), dim3(64), 0, s, a, o, K);
+    if (a.part)  // (nullptr: o was combined by the attention launch itself, attention_decode_comb)
+        hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 63) / 64), dim3(64), 0, s, a, o, K);
     GemvArgs r = a;
     r.x = o;
     r.norm_w = nullptr;

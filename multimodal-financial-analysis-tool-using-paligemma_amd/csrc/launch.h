@@ -80,7 +80,7 @@ bool gemv_qkv_folds_embed(int B);  // batches the fold covers (the register-inpu
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
               uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws = nullptr,
-              const EmbedFold* emb = nullptr, unsigned* arrive = nullptr);
+              const EmbedFold* emb = nullptr);
 // ws: fp32 scratch (>= 4 x B x N floats) for the MFMA path's K split of K = 16384 (B >= 3)
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
               float* ws);
@@ -94,9 +94,7 @@ void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, i
 // n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
                  const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out);
-// decode attention + o_proj (+ residual) in one launch for B <= 2 (kernels_fused.hip); `arrive` is the
-// layer's chunk counter, zeroed by the layer's q|k|v launch (gemv_qkv's `arrive`)
-bool attn_ores_fused(int B);
+
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                 const uint16_t* Wgu, int I, uint16_t* act);
 int gemv_logits_blocks();
@@ -142,8 +140,11 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
 void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
                       int max_chunks);
 constexpr int kAttnChunk = 64;
-void attn_ores(hipStream_t s, int B, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
-               int max_chunks, const uint16_t* Wo, int N, uint16_t* h_inout, unsigned* arrive);
+// B >= 3: flash-decoding whose last-arriving chunk per row combines the row into a.o (bf16 [B][G*256]);
+// cnt: one counter per row (128-B stride), zero between launches (the last arriver re-arms it)
+bool attn_comb_fused(int B);
+void attention_decode_comb(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
+                           int max_chunks, unsigned* cnt);
 constexpr int kAttnPartStride = 16 * 256 + 32;  // floats per (b, kv head, chunk) record
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) k_attn_decode_comb(AttnArgs a, const Step
         last = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)nch;
     __syncthreads();
     if (!last) return;
-    attn_combine_row(part, max_chunks, nch, b, a.G * 256, a.o + (long)b * a.o_b_stride);
+    attn_combine_row(part, max_chunks, nch, b, a.G * 256, a.o);  // o row b at a.o + b * K (o_b_stride == K)
     if (threadIdx.x == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

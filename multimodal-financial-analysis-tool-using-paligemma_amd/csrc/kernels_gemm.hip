@@ -11,6 +11,10 @@
 // are padded to 72 bf16 (144 B) so the 16 rows a ds_read_b128 lane group touches land
 // on distinct banks.  Split-K (grid.z) writes fp32 partial slabs that a separate
 // epilogue kernel reduces in a fixed order (bitwise reproducible).
+#include <map>
+#include <tuple>
+#include <vector>
+
 #include "common.h"
 #include "launch.h"
 
@@ -406,11 +410,31 @@ __device__ __forceinline__ void vm_wait_tiles(int n) {
 // XCD (run x = the blocks lin % 8 == x, in order).  So the n_mt workgroups that read one weight panel
 // sit on one XCD and its L2 serves the panel to all but the first; only panels at a run boundary
 // are fetched by two XCDs.
-__device__ __forceinline__ void xcd_tile(int n_mt, int& mt, int& nt, int& z) {
+//
+// Round 4: when the grid splits into 8 equal blocks of bm row tiles x bn column tiles x bs K slices
+// (the host's xcd_block picks the shape that minimises the bytes each XCD must bring into its L2 --
+// bs/S of K x (bm row panels + bn weight panels) -- and passes it in the high bits of n_mt), XCD x
+// takes block x instead of a run: the batched prefill GEMMs otherwise read the whole activation panel
+// on every XCD (8-image down projection: 718 MB per launch fetched for ≈180 MB of operands).  Inside
+// a block the row tiles of one weight panel stay adjacent.
+__device__ __forceinline__ void xcd_tile(int n_mt_x, int& mt, int& nt, int& z) {
+    const int n_mt = n_mt_x & 1023, xb = n_mt_x >> 10;
     const int S = gridDim.y;
     const int G = gridDim.x * S;
     const int lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const int x = lin & 7, j = lin >> 3, q = G >> 3, r = G & 7;
+    const int x = lin & 7, j = lin >> 3;
+    if (xb) {
+        const int bm = xb & 63, bn = (xb >> 6) & 255, bs = xb >> 14;
+        const int n_nt = G / (n_mt * S);
+        const int gm = n_mt / bm, gn = n_nt / bn;
+        const int xm = x % gm, xn = (x / gm) % gn, xs = x / (gm * gn);
+        const int jm = j % bm, js = (j / bm) % bs, jn = j / (bm * bs);
+        mt = xm * bm + jm;
+        z = xs * bs + js;
+        nt = xn * bn + jn;
+        return;
+    }
+    const int q = G >> 3, r = G & 7;
     const int idx = x * q + (x < r ? x : r) + j;
     mt = idx % n_mt;
     z = (idx / n_mt) % S;
@@ -1196,6 +1220,54 @@ size_t gemm_ws_bytes(int M, int N, int K) {
     return p.split > 1 ? (size_t)p.split * M * N * sizeof(float) : 0;
 }
 
+// host: the XCD block shape for xcd_tile (packed into n_mt's high bits), or 0 for the run order --
+// used only when it cuts the bytes the 8 XCDs must fetch into their L2s by at least 20 %
+static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K);
+static int xcd_block(int n_mt, int n_nt, int S, int BM, int BN, int K) {
+    static const bool off = [] { const char* e = getenv("PGMI_GEMM_XBLK"); return e && atoi(e) == 0; }();
+    if (off) return 0;
+    static std::map<std::tuple<int, int, int, int, int, int>, int> memo;  // (host-side, per launch shape)
+    const auto key = std::make_tuple(n_mt, n_nt, S, BM, BN, K);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+    const int code = xcd_block_pick(n_mt, n_nt, S, BM, BN, K);
+    memo[key] = code;
+    return code;
+}
+
+static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
+    const long G = (long)n_mt * n_nt * S;
+    if (G % 8 != 0 || n_mt >= 1024 || G > 65536) return 0;
+    const double ks = (double)K / S * 2.0;  // bytes per row of one K slice
+    // the run order: XCD x reads the (mt, z) row panels and (nt, z) weight panels of its run
+    const long q = G / 8;
+    double run = 0.0;
+    for (int x = 0; x < 8; ++x) {
+        long na = 0, nb = 0;
+        std::vector<char> sa((size_t)n_mt * S, 0), sb((size_t)n_nt * S, 0);
+        for (long idx = x * q; idx < (x + 1) * q; ++idx) {
+            const int mt = (int)(idx % n_mt), z = (int)((idx / n_mt) % S), nt = (int)(idx / ((long)n_mt * S));
+            if (!sa[(size_t)mt * S + z]++) ++na;
+            if (!sb[(size_t)nt * S + z]++) ++nb;
+        }
+        run += ks * ((double)na * BM + (double)nb * BN);
+    }
+    double best = 0.8 * run;
+    int code = 0;
+    for (int bm = 1; bm <= n_mt && bm < 64; ++bm) {
+        if (n_mt % bm) continue;
+        for (int bn = 1; bn <= n_nt && bn < 256; ++bn) {
+            if (n_nt % bn) continue;
+            for (int bs = 1; bs <= S && bs < 16; ++bs) {
+                if (S % bs || (n_mt / bm) * (n_nt / bn) * (S / bs) != 8) continue;
+                const double bytes = 8.0 * bs * ks * ((double)bm * BM + (double)bn * BN);
+                if (bytes < best) { best = bytes; code = bm | (bn << 6) | (bs << 14); }
+            }
+        }
+    }
+    return code;
+}
+
 template <int WGM, int WGN, int TM, int TN, int EPI>
 static void launch_t(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                      const EpiArgs& ea, float* ws, int split, long up_off) {
@@ -1250,6 +1322,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
     dim3 grid(n_mt * n_nt, split);
+    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>),
@@ -1260,7 +1333,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
     if (EPI < 0 || split > 1) {
         hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
-                           ea, ws, up_off, n_mt, n_nt);
+                           ea, ws, up_off, nmx, n_nt);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1269,7 +1342,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         }
     } else {
         hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, n_mt, n_nt);
+                           per, ea, ws, up_off, nmx, n_nt);
     }
 }
 
@@ -1288,6 +1361,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
     dim3 grid(n_mt * n_nt, split);
+    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>),
@@ -1299,7 +1373,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const dim3 block(64 * (NW + LW));
     if (EPI < 0 || split > 1) {
         hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, n_mt, n_nt);
+                           per, ea, ws, up_off, nmx, n_nt);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1308,7 +1382,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         }
     } else {
         hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, n_mt, n_nt);
+                           per, ea, ws, up_off, nmx, n_nt);
     }
 }
 
@@ -1325,6 +1399,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BNO - 1) / BNO;
     dim3 grid(n_mt * n_nt, split);
+    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, DUAL ? 2 * BNO : BNO, K) << 10);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_8p<TM, EK, false>),
@@ -1335,7 +1410,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
     }
     if (EPI < 0 || split > 1) {
         hipLaunchKernelGGL((k_gemm_8p<TM, EK, true>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
-                           up_off, n_mt);
+                           up_off, nmx);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1344,7 +1419,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
         }
     } else {
         hipLaunchKernelGGL((k_gemm_8p<TM, EK, false>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
-                           up_off, n_mt);
+                           up_off, nmx);
     }
 }
 

@@ -81,6 +81,13 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
     constexpr int NL = RPW * NR * KCW;
     constexpr int K = KCH * 512;
     constexpr int GPB = 4 / WK;    // unit groups per block
+    // the latency-bound projections (q|k|v, o_proj: 18.9 MB a layer) read their weights with the default
+    // cache policy when PGMI_SMALL_NT=0 (probe build): the 4.9 GB of streamed weights stay
+    // non-temporal, so the small ones may stay resident in the Infinity Cache across decode steps
+#ifndef PGMI_SMALL_NT
+#define PGMI_SMALL_NT 1
+#endif
+    constexpr bool kSmallTemporal = !PGMI_SMALL_NT && (MODE == GV_QKV || MODE == GV_ORES);
     __shared__ float red[4][B];
     __shared__ float kred[WK > 1 ? 4 : 1][RPW * NR * B];
 
@@ -112,7 +119,8 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
             for (int j = 0; j < NR; ++j) {
                 const uint16_t* rp = a.W + row_of(u, j) * K + kofs;
 #pragma unroll
-                for (int c = 0; c < KCW; ++c) w[SL][(i * NR + j) * KCW + c] = ldg_nt(rp + 512 * c);
+                for (int c = 0; c < KCW; ++c)
+                    w[SL][(i * NR + j) * KCW + c] = kSmallTemporal ? ldg16(rp + 512 * c) : ldg_nt(rp + 512 * c);
             }
         }
     };

@@ -15,4 +15,4 @@ for i in 1 2; do
     echo "xblk=comb=$v $(tail -n 1 $O/ab.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); c=d["config4_images_per_gpu"]; print(d["value"], d["prefill_ms"], d["prefill_vision_ms"], d["prefill_448"]["prefill_ms"], d["prefill_448"]["prefill_vision_ms"], c["prefill_ms"], c["ms_per_step"])')" >> $O/ab_r4c.txt
   done
 done
-bash tools/gpu_hbm_probe.sh r04
+[ "$1" = hbm ] && bash tools/gpu_hbm_probe.sh r04 || true

@@ -57,9 +57,11 @@ __global__ void __launch_bounds__(256) k_attn_decode_comb(AttnArgs a, const Step
     if (threadIdx.x == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// measured slower than its own combine launch (B = 8 step 1.5585 / 1.5572 -> 1.5832 / 1.5803 ms, same
+// box): off unless PGMI_FUSED_COMB=1 (kept for A/Bs; tests/test_gpu_full_batch.py runs it)
 bool attn_comb_fused(int B) {
-    static const bool off = [] { const char* e = getenv("PGMI_FUSED_COMB"); return e && atoi(e) == 0; }();
-    return !off && B >= 3;
+    static const bool on = [] { const char* e = getenv("PGMI_FUSED_COMB"); return e && atoi(e) != 0; }();
+    return on && B >= 3;
 }
 
 void attention_decode_comb(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,

@@ -1237,6 +1237,10 @@ static int xcd_block(int n_mt, int n_nt, int S, int BM, int BN, int K) {
 
 static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
     const long G = (long)n_mt * n_nt * S;
+    // measured (same box, tools/gpu_r4c.sh): 8-image prefill 12.88 -> 12.59 ms, 448 px flat, but the
+    // 224 px tower 1.46 -> 1.53 ms (its split-K fc2 picked a block order that reads fewer bytes and
+    // runs slower): the block order is used for the batched prefills' activation panels (>= 2048 rows)
+    if ((long)n_mt * BM < 2048) return 0;
     if (G % 8 != 0 || n_mt >= 1024 || G > 65536) return 0;
     const double ks = (double)K / S * 2.0;  // bytes per row of one K slice
     // the run order: XCD x reads the (mt, z) row panels and (nt, z) weight panels of its run

@@ -1,4 +1,6 @@
 // kernels_gemv.hip -- launchers of the decode GEMV kernels (bodies: gemv_body.h).
+#include <cstdlib>
+
 #include "gemv_body.h"
 
 namespace pgmi {
@@ -102,8 +104,10 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
         gemv_mf_ores(s, a, o_out);
         return;
     }
-    // grid capped so each workgroup's combine prologue is amortised over 8 output rows
-    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, 256);
+    // grid capped so each workgroup's combine prologue is amortised over 8 output rows (PGMI_ORES_CAP:
+    // probe knob for same-box sweeps of the cap)
+    static const int cap = [] { const char* e = getenv("PGMI_ORES_CAP"); return e ? atoi(e) : 256; }();
+    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, cap);
     else if (B <= 2) launch_gemv<2, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 4) launch_gemv<4, 4, 1, GV_ORES>(s, a, 256);
     else launch_gemv<8, 4, 1, GV_ORES>(s, a, 256);

@@ -214,14 +214,6 @@ int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* str
  * restores the graphs. */
 int pgmi_prefill_probe(pgmi_ctx* ctx, int on);
 int pgmi_prefill_probe_times(pgmi_ctx* ctx, float* us, int n);
-/* B = 1 decode, one-launch MLP half (PGMI_PERSIST=1; replaces the o_proj, gate|up and down GEMV launches of
- * modeling_gemma.py:293,327-336 with one launch of 256 co-resident workgroups): *active = whether decode steps
- * take it on this device/config, *gave_up = whether any of its bounded hand-off waits timed out since the last
- * call (the flag is cleared).  Synchronises the device. */
-int pgmi_persist_status(pgmi_ctx* ctx, int* active, int* gave_up);
-/* probe: the last one-launch MLP half's per-workgroup phase timestamps (PGMI_PERSIST_DBG=1), 256 x 16 words;
- * returns the words written or < 0 */
-int pgmi_persist_debug(pgmi_ctx* ctx, uint64_t* out, int n);
 /* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent
  * calls (kernels_gemm.hip enum Cfg: 0-5 register-staged tiles, 6-29 LDS-DMA panel tiles, 30-35 warp-specialised panel tiles);
  * cfg < 0 restores the automatic (measured) plan. */

@@ -115,10 +115,6 @@ struct pgmi_ctx {
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
     unsigned* arrive_rows;       // per batch row: chunk counter of the batched attention + combine launch
     hipStream_t cap_stream = nullptr;
-    // B = 1 one-launch MLP half (kernels_persist.hip): hand-off granules, give-up flag, usable here
-    unsigned long long* persist_gran = nullptr;
-    unsigned* persist_err = nullptr;
-    bool persist_ok = false;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
     // identical pointer/shape arguments (a replay is the eager call: kernels read the same
@@ -606,8 +602,6 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->pidx, (size_t)B * gemv_logits_blocks()))) return rc;
         if ((rc = dalloc_t(x, &x->step, 1))) return rc;
         if ((rc = dalloc_t(x, &x->pstep, 1))) return rc;
-        HIPCHK(hipMemset(x->step, 0, sizeof(StepState)));
-        HIPCHK(hipMemset(x->pstep, 0, sizeof(StepState)));
         if ((rc = dalloc_t(x, &x->amax_v, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->amax_i, (size_t)argmax_scratch_parts()))) return rc;
         if ((rc = dalloc_t(x, &x->d_ids, (size_t)B))) return rc;
@@ -621,18 +615,6 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));
-        {
-            int dev = 0, ncu = 0;
-            HIPCHK(hipGetDevice(&dev));
-            HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            x->persist_ok = ncu >= 256 && c.t_hidden == 2048 && c.t_intermediate == 16384 &&
-                            c.t_heads * c.t_head_dim == 2048 && c.t_kv_heads == 1 && c.t_head_dim == 256;
-            const size_t gb = mlp_persist_granule_bytes();
-            if ((rc = dalloc_t(x, &x->persist_gran, gb / 8))) return rc;
-            HIPCHK(hipMemset(x->persist_gran, 0, gb));
-            if ((rc = dalloc_t(x, &x->persist_err, 64))) return rc;
-            HIPCHK(hipMemset(x->persist_err, 0, 64 * sizeof(unsigned)));
-        }
     }
     // derived tensors
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
@@ -994,13 +976,6 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
             attention_decode_comb(s, a, x->step, launch_keys, x->opart, x->max_chunks, x->arrive_rows);
             gemv_o_attn(s, B, NH, nullptr, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
                         x->dAO);
-        } else if (B == 1 && x->persist_ok && mlp_persist_on()) {
-            // o_proj .. down as one launch (kernels_persist.hip)
-            attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
-            mlp_persist(s, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"),
-                        TL(x, i, "mlp.gate_proj.weight"), TL(x, i, "mlp.down_proj.weight"),
-                        TL(x, i, "post_attention_layernorm.weight"), eps, x->dH, x->persist_gran, x->persist_err, i);
-            continue;
         } else {
             attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
             gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
@@ -1053,26 +1028,6 @@ int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
         us[L + i] = b * 1e3f;
     }
     return 0;
-}
-
-int pgmi_persist_status(pgmi_ctx* x, int* active, int* gave_up) {
-    if (!x || !active || !gave_up) return fail(PGMI_E_ARG, "null argument");
-    *active = (x->persist_ok && mlp_persist_on()) ? 1 : 0;
-    *gave_up = 0;
-    if (x->persist_err) {
-        unsigned e = 0;
-        HIPCHK(hipDeviceSynchronize());
-        HIPCHK(hipMemcpy(&e, x->persist_err, sizeof(e), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemset(x->persist_err, 0, sizeof(unsigned)));
-        *gave_up = e != 0;
-    }
-    return 0;
-}
-
-int pgmi_persist_debug(pgmi_ctx* x, uint64_t* out, int n) {
-    if (!x || !out) return fail(PGMI_E_ARG, "null argument");
-    HIPCHK(hipDeviceSynchronize());
-    return mlp_persist_debug(reinterpret_cast<unsigned long long*>(out), n);
 }
 
 int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {

@@ -555,7 +555,6 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                     if (a.adv) {
                         a.adv->kv_len += 1;
                         a.adv->position += 1;
-                        a.adv->epoch += 1;
                     }
                 }
                 if (tid <= NSH) __hip_atomic_store(a.done + tid * STR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

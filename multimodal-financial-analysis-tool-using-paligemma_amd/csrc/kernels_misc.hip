@@ -505,7 +505,6 @@ __global__ void k_argmax_finish(const float* __restrict__ pmax, const int* __res
     if (adv && b == 0 && threadIdx.x == 0) {
         adv->kv_len += 1;
         adv->position += 1;
-        adv->epoch += 1;
     }
     float best = -INFINITY;
     int bi = 0x7fffffff;

@@ -65,7 +65,6 @@ constexpr int kGemmCfgs = 38;              // tile configurations (kernels_gemm.
 struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)
     int kv_len;     // index the new token's K/V is written at (= KVCache.num_items())
     int position;   // rotary position (= attention_mask.cumsum(-1)[:, -1], modeling_gemma.py:526)
-    unsigned epoch; // decode steps run so far (never reset): the hand-off tags of kernels_persist.hip
 };
 
 // decode layer 0: the embedding lookup folded into the q|k|v GEMV (h_out receives the scaled row)
@@ -198,14 +197,6 @@ void patchify(hipStream_t s, const void* px, int px_is_f32, int B, int C, int H,
               uint16_t* out);
 void fill_synthetic(hipStream_t s, uint16_t* dst, long n, uint64_t key, float scale, float offset);
 void set_step(hipStream_t s, StepState* st, int kv_len, int position);
-// B = 1 decode: o_proj (+ attention combine) + residual + RMSNorm + gate|up + GeGLU + down + residual
-// as one launch of 256 co-resident workgroups (kernels_persist.hip); gran: mlp_persist_granule_bytes()
-bool mlp_persist_on();
-size_t mlp_persist_granule_bytes();
-int mlp_persist_debug(unsigned long long* out, int n);
-void mlp_persist(hipStream_t s, const float* part, int max_chunks, const StepState* st, const uint16_t* Wo,
-                 const uint16_t* Wgu, const uint16_t* Wd, const uint16_t* norm_w, float eps, uint16_t* h,
-                 unsigned long long* gran, unsigned* err, int layer);
 // step state with the rotary position read on the device: round(pos[0]) of a (B, 1) position tensor
 // of dtype PGMI_DTYPE_* (+ 10 = int64, 11 = int32, 12 = float64) -- no host read of a merge's positions
 void set_step_dev(hipStream_t s, StepState* st, int kv_len, const void* pos, int dtype);

@@ -71,8 +71,6 @@ SIGNATURES = {
     "pgmi_prefill_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_prefill_probe": (i32, [vp, i32]),
     "pgmi_prefill_probe_times": (i32, [vp, ctypes.POINTER(f32), i32]),
-    "pgmi_persist_status": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
-    "pgmi_persist_debug": (i32, [vp, vp, i32]),
     "pgmi_preprocess": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
     "pgmi_argmax": (i32, [vp, vp, i32, i32, vp, vp]),
     "pgmi_lm_head": (i32, [vp, vp, i32, vp, vp]),

@@ -336,7 +336,7 @@ class GemmaForCausalLM(nn.Module):
         if owner is not None:
             return owner._pgmi_engine()
         _check_tied(self)
-        return _binding.bind(self, _binding.text_cfg(self.config), "language_model.",
+        return _binding.bind(self, lambda: _binding.text_cfg(self.config), "language_model.",
                              inv_freq=self.model.layers[0].self_attn.rotary_emb.inv_freq if self.model.layers else None)
 
     def forward(self, attention_mask: Optional[torch.Tensor] = None, position_ids: Optional[torch.LongTensor] = None,
@@ -368,30 +368,52 @@ def _check_tied(lm: "GemmaForCausalLM"):
 
 class _PaddingCheck:
     """`assert torch.all(attention_mask == 1)` (modeling_gemma.py:558) without a host sync AHEAD of the
-    GPU work: for a device mask the comparison is enqueued first and its result copied to pinned host
+    GPU work: for a device mask the comparison runs on a side stream (behind an event of the caller's
+    stream, so it sees the mask the caller's kernels produced) and its result is copied to pinned host
     memory behind an event; wait() reads it -- raising the reference's AssertionError -- after this
-    call's kernels are enqueued and before any Python-side state (the KVCache length) changes, so the
-    GPU never idles while the host waits for the check."""
+    call's kernels are enqueued and before any Python-side state (the KVCache length) changes.
+    launch() may come after the step's own launch (the KV-cached decode step): the check's host cost
+    then overlaps the step instead of delaying it; nothing is committed before wait()."""
 
     _flags = {}
+    _streams = {}
+    _events = {}  # per device: (the caller-stream event, the side-stream event), reused call after call
 
     def __init__(self, mask: torch.Tensor):
-        self.ev, self.bad = None, False
+        self.mask, self.ev, self.bad, self.flag = mask, None, False, None
         if mask.device.type == "cuda":
-            flag = _PaddingCheck._flags.get(mask.device)
-            if flag is None:
-                flag = _PaddingCheck._flags[mask.device] = torch.zeros((), dtype=torch.bool).pin_memory()
-            flag.copy_((mask != 1).any(), non_blocking=True)
-            self.flag = flag
-            self.ev = torch.cuda.Event()
-            self.ev.record()
+            evs = _PaddingCheck._events.get(mask.device)
+            if evs is None:
+                evs = _PaddingCheck._events[mask.device] = (torch.cuda.Event(), torch.cuda.Event())
+            self.ready, self.done = evs
+            self.ready.record()
         else:
             self.bad = bool((mask != 1).any())
 
+    def launch(self):
+        mask = self.mask
+        if mask.device.type != "cuda" or self.ev is not None:
+            return
+        dev = mask.device
+        flag = _PaddingCheck._flags.get(dev)
+        if flag is None:
+            flag = _PaddingCheck._flags[dev] = torch.zeros((), dtype=torch.bool).pin_memory()
+            _PaddingCheck._streams[dev] = torch.cuda.Stream(device=dev)
+        side = _PaddingCheck._streams[dev]
+        side.wait_event(self.ready)
+        with torch.cuda.stream(side):
+            mask.record_stream(side)
+            flag.copy_((mask != 1).any(), non_blocking=True)
+            self.ev = self.done
+            self.ev.record(side)
+        self.flag = flag
+
     def wait(self):
+        self.launch()
         if self.ev is not None:
             self.ev.synchronize()
             self.bad, self.ev = bool(self.flag), None
+        self.mask = None
         assert not self.bad, "The input cannot be padded"
 
 
@@ -464,7 +486,7 @@ class PaliGemmaForConditionalGeneration(nn.Module):
     def _pgmi_engine(self):
         _check_tied(self.language_model)
         layers = self.language_model.model.layers
-        return _binding.bind(self, _pgmi_cfg(self.config), "",
+        return _binding.bind(self, lambda: _pgmi_cfg(self.config), "",
                              inv_freq=layers[0].self_attn.rotary_emb.inv_freq if len(layers) else None)
 
     def _merge_input_ids_with_image_features(self, image_features: torch.Tensor, inputs_embeds: torch.Tensor,
@@ -518,6 +540,10 @@ class PaliGemmaForConditionalGeneration(nn.Module):
         if attention_mask is None:
             raise ValueError("attention_mask must be provided")
         chk = _PaddingCheck(attention_mask)
+        decode_step = (kv_cache is not None and inputs_embeds is None and input_ids is not None and
+                       kv_cache.num_items() > 0 and not self._merge_is_patched())
+        if not decode_step:
+            chk.launch()
         if inputs_embeds is None and input_ids is None:
             chk.wait()
             raise ValueError("You must provide either input_ids or inputs_embeds")
@@ -582,7 +608,9 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             position = int(attention_mask.shape[-1])  # cumsum of an all-ones mask, :526
             slab = kv_cache._ensure(eng, B, cache_len + 1)
             logits = eng.decode(input_ids, slab, cache_len, position, logits=eng.logits_buffer(B),
-                                graph=self.pgmi_use_graph).clone().unsqueeze(1)
+                                graph=self.pgmi_use_graph)
+            chk.launch()  # behind the step's launch: its host cost overlaps the step
+            logits = logits.clone().unsqueeze(1)
             chk.wait()
             kv_cache._len = cache_len + 1
 

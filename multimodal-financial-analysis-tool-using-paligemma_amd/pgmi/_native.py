@@ -155,4 +155,8 @@ def safetensors_index(path: str):
 
 
 def stream_handle(device=None) -> int:
+    """The caller's current HIP stream on `device` (the raw handle, read without building a Stream object:
+    this runs once per engine call, on the decode loop's host path)."""
+    if isinstance(device, torch.device) and device.index is not None:
+        return torch._C._cuda_getCurrentRawStream(device.index)
     return torch.cuda.current_stream(device).cuda_stream

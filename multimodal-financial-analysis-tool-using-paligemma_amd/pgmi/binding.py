@@ -66,17 +66,22 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
     (storage pointer, in-place version, dtype): an in-place update (load_state_dict, copy_) re-binds.
     The sampled parameter objects are kept, so the check costs ~17 attribute reads instead of a
     walk of the module tree (~0.4-0.8 ms per decode step at the 3B shapes); replacing Parameter
-    objects after the first forward needs unbind(module) (PaliGemmaForConditionalGeneration.pgmi_rebind)."""
-    dev = _device_of(module)
+    objects after the first forward needs unbind(module) (PaliGemmaForConditionalGeneration.pgmi_rebind).
+    `cfg` may be a callable returning the config dict (built only when an engine is built).  A bound
+    module's device is its sampled parameters' (a move to another device re-points them: the
+    fingerprint changes), so the per-forward check walks no module tree."""
     b = module.__dict__.get("_pgmi_bound")
     inv_fp = _inv_fingerprint(inv_freq)
-    if b is not None and b.fp == _fingerprint_of(b.sample) and b.engine.device == dev:
+    if b is not None and b.fp == _fingerprint_of(b.sample) and b.sample[0].device == b.engine.device:
         if b.inv_fp != inv_fp:
             # the rotary inv_freq buffer changed (e.g. model.to(dtype) casts it, as the ablation's
             # run_inference does, ablation_study_fixed.py:182): rebuild the RoPE table from its values
             b.engine.prepare(inv_freq=inv_freq)
             b.inv_fp = inv_fp
         return b.engine
+    dev = _device_of(module)
+    if callable(cfg):
+        cfg = cfg()
     eng = Engine(cfg, device=dev, max_batch=DEFAULT_MAX_BATCH, max_seq=DEFAULT_MAX_SEQ)
     with torch.no_grad():
         for name, p in module.named_parameters():

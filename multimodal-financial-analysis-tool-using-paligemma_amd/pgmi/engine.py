@@ -278,7 +278,9 @@ class Engine:
                next_ids: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
         """One KV-cached decode step for B sequences; returns logits (B, V) fp32."""
         self._ready()
-        ids = ids.to(self.device, torch.int64).reshape(-1).contiguous()
+        if ids.dtype is not torch.int64 or ids.device != self.device or not ids.is_contiguous():
+            ids = ids.to(self.device, torch.int64).contiguous()
+        ids = ids.view(-1)
         B = ids.numel()
         if logits is None:
             logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)

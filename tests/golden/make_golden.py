@@ -22,6 +22,7 @@ What is captured:
                     patches): KV mode 64 tokens incl. the step-0 prompt re-feed, no-KV mode 48 tokens
   full_batch8_bf16.npz  configs[3]: 8 distinct images, each run alone through inference.test_inference
   full_batch8_fp32.npz  the fp32 truth of each of those 8 rows, teacher-forced on its bf16 token path
+  full448_decode_{bf16,fp32}.npz  448 px (L = 1056): 16 greedy KV-cached tokens and their fp32 truth
 """
 from __future__ import annotations
 
@@ -454,6 +455,42 @@ def make_long(pixels, n_tokens=256):
     print("full256_{bf16,fp32}.npz written")
 
 
+def make_448_decode(pixels, n_tokens=16):
+    """configs[4]'s shapes (448 px, L = 1056) through the KV-cached decode loop: n_tokens greedy tokens
+    via inference.test_inference (step 0 is the prefill's last row), then the fp32 truth teacher-forced
+    on the same token path (pixel_values at step 0 only: the later steps' image features are discarded
+    by the merge, modeling_gemma.py:509-531)."""
+    cfg = W.full_config(448)
+    V = cfg["text_config"]["vocab_size"]
+    sidx = sample_idx(V)
+    ids = prompt_ids(cfg)
+    model, _ = build_model(cfg, torch.bfloat16)
+    t0 = time.time()
+    toks, step_logits = run_test_inference(model, cfg, ids, COCO[0], n_tokens)
+    toks = toks.reshape(-1)
+    print(f"448 bf16 greedy {n_tokens} tokens in {time.time() - t0:.1f}s: {toks.tolist()}")
+    np.savez_compressed(os.path.join(HERE, "full448_decode_bf16.npz"), ids=ids, tokens=toks, sample_idx=sidx,
+                        **summarize_steps(step_logits, sidx))
+    del model
+    model, _ = build_model(cfg, torch.float32)
+    px = torch.from_numpy(pixels["px_0_448"][None])
+    kv = RG.KVCache()
+    mask = torch.ones((1, ids.shape[1]), dtype=torch.int64)
+    cur = torch.from_numpy(ids)
+    fl = []
+    t0 = time.time()
+    with torch.no_grad():
+        for step in range(n_tokens):
+            out = model(input_ids=cur, pixel_values=px if step == 0 else None, attention_mask=mask, kv_cache=kv)
+            fl.append(out["logits"][:, -1, :].float().numpy()[:, sidx])
+            cur = torch.tensor([[int(toks[step])]])
+            mask = torch.cat([mask, torch.ones((1, 1))], dim=-1)
+    fl = np.concatenate(fl, 0)
+    print(f"448 fp32 teacher-forced {n_tokens} steps in {time.time() - t0:.1f}s")
+    np.savez_compressed(os.path.join(HERE, "full448_decode_fp32.npz"), sample_idx=sidx, sample_vals=fl)
+    print("full448_decode_{bf16,fp32}.npz written")
+
+
 def make_ablation(n_kv=64, n_nokv=48, small=False):
     """The paper's own harness (ablation_study_fixed.py:168-287 run_inference) on the reference model
     with BOTH of load_model_simple's patches applied (:335-342: the merge and every layer's rotary
@@ -519,7 +556,7 @@ def make_ablation(n_kv=64, n_nokv=48, small=False):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation"], default=None,
+    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation", "448decode"], default=None,
                     help="generate only one later round's fixtures (full_batch8 / full256 / full_ablation)")
     a = ap.parse_args()
     torch.set_num_threads(8)
@@ -534,6 +571,8 @@ if __name__ == "__main__":
         make_ablation()
     elif a.only == "long":
         make_long(px)
+    elif a.only == "448decode":
+        make_448_decode(px)
     else:
         make_small(px)
         if not a.skip_full:

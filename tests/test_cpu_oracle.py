@@ -208,3 +208,18 @@ def test_batch8_fp32_fixture_consistency(golden_dir):
         e = np.mean([np.linalg.norm(b8["sample_vals"][r, t] - f8["sample_vals"][r, t]) /
                      np.linalg.norm(f8["sample_vals"][r, t]) for t in range(f8["sample_vals"].shape[1])])
         assert 1e-3 < e < 5e-2, (r, e)
+
+
+def test_448_decode_fixture_consistency(golden_dir):
+    """full448_decode_{bf16,fp32}.npz: its step 0 is the 448 px prefill fixture bit for bit (same ids,
+    pixels and weights), its tokens are the stored top-1, and the reference bf16 sits 1e-3..2e-2 from
+    its fp32 truth at every step."""
+    p = np.load(os.path.join(golden_dir, "full448_bf16.npz"))
+    b = np.load(os.path.join(golden_dir, "full448_decode_bf16.npz"))
+    f = np.load(os.path.join(golden_dir, "full448_decode_fp32.npz"))
+    assert np.array_equal(p["ids"], b["ids"]) and np.array_equal(p["sample_idx"], b["sample_idx"])
+    assert np.array_equal(p["sample_vals"][0], b["sample_vals"][0])
+    assert np.array_equal(b["topk_idx"][:, 0], b["tokens"].reshape(-1))
+    assert f["sample_vals"].shape == b["sample_vals"].shape == (16, b["sample_idx"].shape[0])
+    e = np.linalg.norm(b["sample_vals"] - f["sample_vals"], axis=1) / np.linalg.norm(f["sample_vals"], axis=1)
+    assert 1e-3 < e.min() and e.max() < 2e-2, e

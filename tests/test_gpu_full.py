@@ -29,7 +29,8 @@ def G(golden_dir):
     load = lambda n: np.load(os.path.join(golden_dir, n))  # noqa: E731
     return {"bf16": load("full_bf16.npz"), "fp32": load("full_fp32.npz"), "nokv": load("full_nokv_bf16.npz"),
             "448": load("full448_bf16.npz"), "px": load("pixels.npz"), "bf16_256": load("full256_bf16.npz"),
-            "fp32_256": load("full256_fp32.npz")}
+            "fp32_256": load("full256_fp32.npz"), "448d": load("full448_decode_bf16.npz"),
+            "448d_fp32": load("full448_decode_fp32.npz")}
 
 
 def _engine(image_size, max_seq=320, max_kv=576):
@@ -52,13 +53,13 @@ def _px(G, key):
     return torch.from_numpy(pixels_from_u8(G["px"][key])[None]).cuda()
 
 
-def _teacher_forced(e, G, gb, gf, n):
+def _teacher_forced(e, G, gb, gf, n, px_key="u8_0_224", kv_cap=576, label="full224"):
     ids = torch.from_numpy(gb["ids"]).cuda()
     L = ids.shape[1]
     ref_toks = gb["tokens"].reshape(-1)
     sidx = torch.from_numpy(gb["sample_idx"]).cuda()
-    kv = e.new_kv(1, 576)
-    feats = e.project(e.vision(_px(G, "u8_0_224")))
+    kv = e.new_kv(1, kv_cap)
+    feats = e.project(e.vision(_px(G, px_key)))
     lg = e.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)[:, 0]
     steps_logits = [lg]
     for t in range(1, n):
@@ -76,7 +77,7 @@ def _teacher_forced(e, G, gb, gf, n):
     assert np.array_equal(am[decisive], ref_toks[decisive]), (am, ref_toks)
     # per-step closeness to the reference bf16 (against its own fp32 floor) and our
     # error vs the fp32 truth relative to the reference's own bf16 error
-    check_model_parity(f"full224/teacher_forced_{n}", ours_s, gb["sample_vals"][:n], gf["sample_vals"][:n])
+    check_model_parity(f"{label}/teacher_forced_{n}", ours_s, gb["sample_vals"][:n], gf["sample_vals"][:n])
 
 
 @torch.no_grad()
@@ -140,11 +141,21 @@ def test_prefill_448(G):
         top = torch.gather(lg, 0, torch.from_numpy(g["topk_idx"][0]).cuda()).cpu().numpy()
         assert np.abs(top - g["topk_val"][0]).max() <= 0.25, rows
         s = lg[torch.from_numpy(g["sample_idx"]).cuda()].cpu().numpy()
-        # no fp32 truth exists for the 448 px fixture: the 224 px floor (2.4e-2 at the prefill
-        # step) is what the 3e-2 bound covers
-        st = logit_stats(f"full448/prefill_rows{rows}", s[None], g["sample_vals"][:1])
-        assert st["rel_vs_ref_bf16_max"] < 3e-2, rows
+        # the fp32 truth of this prefill step is step 0 of full448_decode_fp32.npz (same ids, pixels
+        # and weights: its bf16 step 0 equals this fixture exactly): the SURVEY sec.8c rule
+        check_model_parity(f"full448/prefill_rows{rows}", s[None], g["sample_vals"][:1],
+                           G["448d_fp32"]["sample_vals"][:1])
         if g["margin"][0] > 0.25:
             assert int(lg.argmax()) == int(g["topk_idx"][0, 0]), rows
     del e
     torch.cuda.empty_cache()
+
+
+@torch.no_grad()
+def test_decode_448_teacher_forced(G):
+    """configs[4]'s shapes through the KV-cached decode loop: the 448 px prefill (L = 1056) and 15
+    graph-replayed decode steps over 1057..1071 cached keys (17 flash-decoding chunks: past the
+    12-chunk register form of the o_proj prologue's combine), teacher-forced on the reference's
+    16 greedy tokens (tests/golden/full448_decode_*.npz), under the same rules as 224 px."""
+    e = _engine(448, max_seq=1088, max_kv=1088)
+    _teacher_forced(e, G, G["448d"], G["448d_fp32"], 16, px_key="u8_0_448", kv_cap=1088, label="full448")

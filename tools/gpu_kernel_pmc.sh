@@ -37,3 +37,5 @@ echo done
 PGMI_ROUND=$TAG python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     "k_gemv<1, 4, 1, 2, 1, true, 1, false>" gateup $OUT/pmc_traffic.json >> $OUT/summary.txt
 echo traffic done
+python3 $R/tools/prefill_gemm_shapes.py $OUT/trace/run_kernel_trace.csv $OUT/prefill_gemm_shapes.csv >> $OUT/summary.txt
+echo shapes done

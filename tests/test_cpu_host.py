@@ -196,3 +196,31 @@ def test_ablation_patches_restated_match_reference_semantics():
     assert torch.equal(out[0, :, 0], torch.tensor([1.0, 1.0, 1.0, 0.0, 1.0]))  # 2 / sqrt(4) = 1; pad row zero
     out, mask, pos = ablation_merge(self, img, emb, ids, torch.ones(1, 12, dtype=torch.long)[:, :5], None)
     assert mask.shape == (1, 1, 5, 5) and pos.tolist() == [[0, 1, 2, 3, 4]]
+
+
+def test_prefill_gemm_shape_labels(tmp_path):
+    """tools/prefill_gemm_shapes.py splits one kernel template's launches by shape: a W128x128 split launch
+    after the GeGLU GEMM (or after another one: bench.py's back-to-back graph) is the down projection, any
+    other is o_proj -- the per-shape figures bench.py's in-situ prefill_gemm_roofline is checked against."""
+    import csv
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("pgs", os.path.join(root, "tools", "prefill_gemm_shapes.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    seq = [("k_attn_fs", 5), (m.W128S, 10), ("k_splitk", 3), (m.GU224, 44), (m.W128S, 36), ("k_splitk", 3),
+           (m.GU224, 44), (m.W128S, 36), (m.W128S, 38), ("x", 1), (m.GU448, 126), (m.DN448, 72)]
+    tr = tmp_path / "trace.csv"
+    with open(tr, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        t = 0
+        for name, us in seq:
+            w.writerow([f"void pgmi::{name}(args)", t, t + us * 1000])
+            t += us * 1000 + 500
+    out = tmp_path / "out.csv"
+    m.main(str(tr), str(out))
+    rows = {r["label"]: r for r in csv.DictReader(open(out))}
+    assert rows["224 o_proj (M=288)"]["launches"] == "1" and float(rows["224 o_proj (M=288)"]["mean_us"]) == 10
+    assert rows["224 down (M=288)"]["launches"] == "3" and float(rows["224 down (M=288)"]["median_us"]) == 36
+    assert float(rows["448 gate|up + GeGLU (M=1056)"]["mean_us"]) == 126

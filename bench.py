@@ -206,7 +206,8 @@ def gemm_roofline(eng, rows, iters=36, reps=4):
 def gemm_insitu(eng, px, ids, pos, kv, reps=3):
     """The same GEMMs timed in situ: pgmi_prefill_probe brackets every layer's gate|up and down GEMM
     with HIP events inside eager LM prefills (logits_rows 1: every layer runs its MLP GEMMs); the median
-    over reps x 18 layers."""
+    over reps x 18 layers.  The events are the GEMM kernel's own (hipExtLaunchKernelGGL start / stop:
+    the kernel's execution alone, as a kernel trace times it, not the stream's packets around it)."""
     import ctypes
     import torch
     from pgmi import _native as N
@@ -238,8 +239,8 @@ def with_insitu(iso, gu_us, dn_us):
         out[name] = {"bound": "mfma", "rows": e["rows"], "flop_per_launch": e["flop_per_launch"],
                      "avg_launch_us": round(us, 2), "achieved": round(tfs, 1), "peak": MFMA_BF16_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": round(tfs / MFMA_BF16_PEAK_TFS, 4),
-                     "timing": "in situ: HIP events around the GEMM in eager LM prefills (pgmi_prefill_probe), "
-                               "median over the 18 layers x 3 forwards",
+                     "timing": "in situ: the GEMM kernel's own start/stop events (hipExtLaunchKernelGGL) in eager "
+                               "LM prefills (pgmi_prefill_probe), median over the 18 layers x 3 forwards",
                      "isolated": {k: e[k] for k in ("avg_launch_us", "achieved", "frac", "timing")}}
     return out
 

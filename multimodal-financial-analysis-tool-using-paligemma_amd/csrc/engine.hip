@@ -896,16 +896,15 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
         EpiArgs g{};
         g.out = x->ACT; g.ldo = c.t_intermediate;
         const bool probe = x->probe_on && (size_t)(4 * i + 3) < x->probe_ev.size();
-        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i], s));
+        // probe: the GEMM kernel itself carries the events (its own start / end, gemm_probe_events)
+        if (probe) gemm_probe_events(x->probe_ev[4 * i], x->probe_ev[4 * i + 1]);
         gemm(s, x->Tn, H, TL(x, i, "mlp.gate_proj.weight"), H, R, c.t_intermediate, H, EPI_GEGLU, g, x->ws,
              x->ws_bytes, c.t_intermediate);
-        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 1], s));
         EpiArgs d{};
         d.res = x->Hs; d.ldr = H; d.out = x->Hs; d.ldo = H;
-        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 2], s));
+        if (probe) gemm_probe_events(x->probe_ev[4 * i + 2], x->probe_ev[4 * i + 3]);
         sp = gemm(s, x->ACT, c.t_intermediate, TL(x, i, "mlp.down_proj.weight"), c.t_intermediate, R, H,
                   c.t_intermediate, EPI_RES, d, x->ws, x->ws_bytes, 0, true);
-        if (probe) HIPCHK(hipEventRecord(x->probe_ev[4 * i + 3], s));
         const bool last = i + 1 == c.t_layers;
         splitk_res_norm(s, x->ws, sp, nullptr, x->Hs, last ? fnorm : TL(x, i + 1, "input_layernorm.weight"), nullptr,
                         eps, x->Tn, R, H);

@@ -15,6 +15,8 @@
 #include <tuple>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 #include "launch.h"
 
@@ -1272,6 +1274,24 @@ static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
     return code;
 }
 
+// in-situ timing probe (pgmi_prefill_probe): when a pair of events is armed, the next GEMM kernel is
+// launched with hipExtLaunchKernelGGL, whose events take that kernel's own start and end -- a time
+// free of the host's launch pace and of the stream's other packets; the pair is used once
+static hipEvent_t g_probe_ev0 = nullptr, g_probe_ev1 = nullptr;
+void gemm_probe_events(hipEvent_t start, hipEvent_t stop) {
+    g_probe_ev0 = start;
+    g_probe_ev1 = stop;
+}
+#define PGMI_GEMM_LAUNCH(KERN, GRID, BLOCK, LDS, S, ...)                                                  \
+    do {                                                                                                \
+        if (g_probe_ev0) {                                                                              \
+            hipExtLaunchKernelGGL(KERN, GRID, BLOCK, LDS, S, g_probe_ev0, g_probe_ev1, 0, __VA_ARGS__); \
+            g_probe_ev0 = g_probe_ev1 = nullptr;                                                        \
+        } else {                                                                                        \
+            hipLaunchKernelGGL(KERN, GRID, BLOCK, LDS, S, __VA_ARGS__);                                 \
+        }                                                                                               \
+    } while (0)
+
 template <int WGM, int WGN, int TM, int TN, int EPI>
 static void launch_t(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                      const EpiArgs& ea, float* ws, int split, long up_off) {
@@ -1291,14 +1311,14 @@ static void launch_t(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         attr_set = true;
     }
     if constexpr (EPI < 0) {
-        hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, EPI_STORE, true>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N,
+        PGMI_GEMM_LAUNCH((k_gemm<WGM, WGN, TM, TN, EPI_STORE, true>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N,
                            K, per, ea, ws, up_off);
         return;
     } else if (split == 1) {
-        hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, EPI, false>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm<WGM, WGN, TM, TN, EPI, false>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off);
     } else {
-        hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, EPI_STORE, true>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N,
+        PGMI_GEMM_LAUNCH((k_gemm<WGM, WGN, TM, TN, EPI_STORE, true>), grid, dim3(NT), lds, s, A, lda, W, ldw, M, N,
                            K, per, ea, ws, up_off);
         long total4 = ((long)M * N + 3) / 4;
         long blocks = (total4 + 255) / 256;
@@ -1336,7 +1356,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         attr_set = true;
     }
     if (EPI < 0 || split > 1) {
-        hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
+        PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
                            ea, ws, up_off, nmx, n_nt);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
@@ -1345,7 +1365,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
             hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
         }
     } else {
-        hipLaunchKernelGGL((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, nmx, n_nt);
     }
 }
@@ -1376,7 +1396,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
     const dim3 block(64 * (NW + LW));
     if (EPI < 0 || split > 1) {
-        hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, nmx, n_nt);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
@@ -1385,7 +1405,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
             hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
         }
     } else {
-        hipLaunchKernelGGL((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, nmx, n_nt);
     }
 }
@@ -1413,7 +1433,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
         attr_set = true;
     }
     if (EPI < 0 || split > 1) {
-        hipLaunchKernelGGL((k_gemm_8p<TM, EK, true>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
+        PGMI_GEMM_LAUNCH((k_gemm_8p<TM, EK, true>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
                            up_off, nmx);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
@@ -1422,7 +1442,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
             hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
         }
     } else {
-        hipLaunchKernelGGL((k_gemm_8p<TM, EK, false>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
+        PGMI_GEMM_LAUNCH((k_gemm_8p<TM, EK, false>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
                            up_off, nmx);
     }
 }

@@ -59,6 +59,8 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
 size_t gemm_ws_bytes(int M, int N, int K);
 void gemm_force_plan(int cfg, int split);  // cfg < 0: automatic
 int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split);  // cfg < 0: remove the override
+// probe: the next GEMM kernel launched takes these events as its own start / stop (hipExtLaunchKernelGGL)
+void gemm_probe_events(hipEvent_t start, hipEvent_t stop);
 constexpr int kGemmCfgs = 38;              // tile configurations (kernels_gemm.hip Cfg)
 
 // ---------------------------------------------------------------- decode GEMV

@@ -208,8 +208,9 @@ int pgmi_preprocess(pgmi_ctx* ctx, const void* src_hwc, int H, int W, int out_h,
 int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* stream);
 
 /* In-situ timing probe of the prefill MLP GEMMs (measurement only): on != 0 makes every following
- * pgmi_lm_forward eager (prefill graphs off) and brackets each layer's gate|up + GeGLU GEMM and down
- * GEMM (modeling_gemma.py:133-134) with HIP events; pgmi_prefill_probe_times writes the last probed
+ * pgmi_lm_forward eager (prefill graphs off) and times each layer's gate|up + GeGLU GEMM and down
+ * GEMM kernel (modeling_gemma.py:133-134) with its own start / stop events (hipExtLaunchKernelGGL: the
+ * kernel's execution alone); pgmi_prefill_probe_times writes the last probed
  * forward's durations in microseconds: us[i] = layer i's gate|up, us[layers + i] = its down.  on = 0
  * restores the graphs. */
 int pgmi_prefill_probe(pgmi_ctx* ctx, int on);

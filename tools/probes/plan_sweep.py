@@ -52,7 +52,9 @@ def time_lm(eng, args, iters):
 
 
 # a candidate is eligible only when its output matches the default plan's (a broken candidate,
-# e.g. one whose split leaves a K range unwritten, must not win on time alone)
+# e.g. one whose split leaves a K range unwritten, must not win on time alone).  Two correct plans that
+# differ only in accumulation order land ~1.1e-2 (tower) / ~1.7e-2 (LM logits) apart after the layer
+# stack; --rel-tol 5e-2 admits them while still rejecting a broken one (rel-L2 ~1)
 REL_TOL = 1e-2
 
 
@@ -80,7 +82,9 @@ def main():
     ap.add_argument("--px", type=int, default=224, choices=[224, 448])
     ap.add_argument("--cfgs", default=None, help="candidate tile configs (default: CFGS / CFGS_LM)")
     ap.add_argument("--splits", default=None, help="candidate K splits (default: per shape)")
+    ap.add_argument("--rel-tol", type=float, default=REL_TOL, help="eligibility bound (rel-L2 vs the default plan)")
     a = ap.parse_args()
+    globals()["REL_TOL"] = a.rel_tol
     if a.cfgs:
         CFGS[:] = CFGS_LM[:] = [int(c) for c in a.cfgs.split(",")]
     cfg = paligemma_3b_config(a.px)

@@ -1173,7 +1173,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {1056, 2560, 2048, false, W128x128, 1}, // 448 px text q|k|v     21.3 us (P96x64s3 24.0 in the same sweep)
         {1056, 2048, 2048, false, W128x128, 1}, // 448 px text o_proj    19.5 us (P96x64s3 23.9)
         {1056, 16384, 2048, true, E192, 1},     // 448 px gate|up       135.5 us (W352w 149.8); in situ LM 5688 -> 5538 us
-        {1056, 2048, 16384, false, E192, 4},    // 448 px down          (W288w split 4 79.1 us); in situ 5688 -> 5539 us
+        {1056, 2048, 16384, false, E192, 5},    // 448 px down          (W288w split 4 79.1 us); in situ 5688 -> 5539 us;
+                                                // round 4 in situ (profiles/r04_plan_sweeps.txt): split 5 (240 WGs) 5294 -> 5271 us
         {1024, 3456, 1152, false, W128x128, 1}, // 448 px vision q|k|v   18.3 us (was 24.6)
         {1024, 1152, 1152, false, P96x64s4, 1}, // 448 px vision out     10.6 us (P32x64s4 13.7)
         {1024, 4304, 1152, false, W288w, 1},    // 448 px vision fc1     25.1 us (exp/rcp GELU; was 29.5)

@@ -717,6 +717,10 @@ def main():
             "vs_baseline_note": "BASELINE.md publishes no number for this hardware/dtype; its only decode figure is "
                                 "10.17 tok/s per GPU (RTX 2060, fp16, KV cache, 256 tokens)",
             "per_gpu_tok_s": round(tok_s / world, 3),
+            # N > 1 runs configs[3] (8 images per GPU), N = 1 configs[1] (batch 1): the like-for-like single-GPU
+            # figure for a scaling ratio of the N > 1 lines is the N = 1 line's config4_images_per_gpu leg
+            "scaling_reference": ("config4_images_per_gpu.decode_tok_s of the N = 1 line (the same per-GPU work: "
+                                  "8 images)" if world > 1 else None),
             "dtype": "bf16",
             "data": "synthetic (deterministic random-init PaliGemma-3B weights, seeded random 224x224 images, "
                     "synthetic 32-token prompt)",

@@ -212,7 +212,8 @@ int pgmi_prefill_kernel(pgmi_ctx* ctx, int which, int layer, int rows, void* str
  * GEMM kernel (modeling_gemma.py:133-134) with its own start / stop events (hipExtLaunchKernelGGL: the
  * kernel's execution alone); pgmi_prefill_probe_times writes the last probed
  * forward's durations in microseconds: us[i] = layer i's gate|up, us[layers + i] = its down.  on = 0
- * restores the graphs. */
+ * restores the graphs.  Probe with logits_rows 0 or 1: under logits_rows 2 the last layer's MLP runs on the
+ * decode GEMVs (no GEMM to time) and pgmi_prefill_probe_times returns PGMI_E_HIP (the unset events). */
 int pgmi_prefill_probe(pgmi_ctx* ctx, int on);
 int pgmi_prefill_probe_times(pgmi_ctx* ctx, float* us, int n);
 /* Tuning hook: force the prefill GEMM tile configuration and split-K factor for subsequent

@@ -429,3 +429,36 @@ def test_decode_embeds_dev_position_and_mask(eng, gold, mask_dtype):
     top = np.argsort(ref)[-8:]
     assert np.abs(got[top] - ref[top]).max() <= 0.25
     assert rel_l2(got, host.cpu().numpy()[0]) > 1e-3  # the mask changed the step
+
+
+@torch.no_grad()
+def test_prefill_probe_kernel_events(eng, gold):
+    """pgmi_prefill_probe (bench.py's in-situ GEMM timing): every layer's gate|up and down GEMM kernel takes
+    its own start / stop events; the probed (eager) forward returns the same logits as the unprobed one,
+    every time is positive and below a bound, and switching the probe off restores the graphs.  logits_rows 1
+    (every layer's MLP on every row, as bench.py probes it): with 2 the last layer's MLP runs for the last row
+    on the decode GEMVs, so it has no GEMM to time and pgmi_prefill_probe_times reports an error."""
+    import ctypes
+
+    from pgmi import _native as N
+    ids = torch.from_numpy(gold["ids"]).cuda()
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    feats = eng.project(eng.vision(px))
+    L = ids.shape[1]
+    kv = eng.new_kv(1, 512)
+    pos = torch.arange(L)[None]
+    ref = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1).clone()
+    nl = W.small_config()["text_config"]["num_hidden_layers"]
+    us = (ctypes.c_float * (2 * nl))()
+    N.check(eng.lib.pgmi_prefill_probe(eng.ctx, 1))
+    try:
+        out = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1).clone()
+        torch.cuda.synchronize()
+        N.check(eng.lib.pgmi_prefill_probe_times(eng.ctx, us, 2 * nl))
+    finally:
+        N.check(eng.lib.pgmi_prefill_probe(eng.ctx, 0))
+    assert torch.equal(out, ref)
+    t = list(us)
+    assert all(1.0 < v < 5000.0 for v in t), t
+    again = eng.lm_forward(kv, 0, pos, ids=ids, image_feats=feats, logits_rows=1)
+    assert torch.equal(again, ref)

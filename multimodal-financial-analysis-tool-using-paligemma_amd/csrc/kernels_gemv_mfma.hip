@@ -11,7 +11,7 @@
 //     it further for the 16384-wide down_proj (fp32 partial slabs, reduced by k_mf_combine);
 //   - B operand (weights) straight from HBM in the MFMA layout: lane (n = lane & 15, g = lane >> 4)
 //     reads 16 B of row n at k = 32i + 8g, so one load instruction covers 64 contiguous bytes of
-//     each of its 16 rows (non-temporal);
+//     each of its 16 rows (default cache policy: the other half of each 128-B line follows; PGMI_MF_NT);
 //   - A operand (activations, B x K bf16): the wave's K slice held in registers, staged through
 //     LDS (row stride K + 8: conflict-free 16-B reads) with the RMSNorm (modeling_gemma.py:114-120)
 //     fused in, or read from global (o_proj's and down_proj's inputs);
@@ -103,10 +103,19 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
 // compiler's in-order vmcnt keeps the second stream in flight across the first's wait.
 // NS (no staging): the q|k|v / gate|up input is already RMSNorm'd (k_rows_norm / k_mf_combine_norm
 // wrote it), so each wave reads its K slice straight from global like the residual projections
+// Weight-stream cache policy of the register-streamed MFMA GEMVs.  Each load instruction reads 64-B
+// halves of 128-B lines (16 rows x 4 lanes of 16 B), the other half following one instruction later:
+// with the default policy the line is kept in L2 for it.  Same-box A/B (B = 8 step, tools/ab_variants.sh
+// b8): non-temporal everywhere 1.551 / 1.556 ms, default policy on gate|up only 1.530 / 1.526, on every
+// mode 1.472 / 1.475.  Probe builds: -DPGMI_MF_NT=1 non-temporal everywhere, 0 gate|up only.
+#ifndef PGMI_MF_NT
+#define PGMI_MF_NT 2
+#endif
 template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false>
 __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restrict__ ws) {
     constexpr int NKB = KW / 128;          // 128-wide k blocks per wave
     constexpr bool STAGE = (MODE != GV_RES) && !NS;
+    constexpr bool kNt = PGMI_MF_NT == 1 || (PGMI_MF_NT == 0 && MODE != GV_GEGLU);
     extern __shared__ __attribute__((aligned(16))) uint16_t mfs[];
     __shared__ float red[MF_MAXB * 16];
     __shared__ f32x4 kred[WK][NR][64];
@@ -140,7 +149,8 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) w[j][kb][i] = ldg_nt(rp + kb * 128 + 32 * i);
+                for (int i = 0; i < 4; ++i)
+                    w[j][kb][i] = kNt ? ldg_nt(rp + kb * 128 + 32 * i) : ldg16(rp + kb * 128 + 32 * i);
         }
     };
     if constexpr (PF == 2) {
@@ -154,7 +164,8 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) dst[kb][i] = ldg_nt(rp + step * (kb * 128 + 32 * i));
+                for (int i = 0; i < 4; ++i)
+                    dst[kb][i] = kNt ? ldg_nt(rp + step * (kb * 128 + 32 * i)) : ldg16(rp + step * (kb * 128 + 32 * i));
         };
         const int G = gridDim.x;
         // activation rows n >= nb re-read row nb - 1 (unconditional loads): they only feed C rows

@@ -371,6 +371,12 @@ __device__ __forceinline__ void mf_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS-DMA cache policy of the ring's weight stream: non-temporal (aux 2).  Its 256-B row segments are whole
+// lines read once; same-box A/B (B = 8 step, the batched lm_head's ring): default policy 1.4723 / 1.4730 ms,
+// non-temporal 1.4580 / 1.4565 ms.  Probe build -DPGMI_ML_AUX=0 for the default policy.
+#ifndef PGMI_ML_AUX
+#define PGMI_ML_AUX 2
+#endif
 template <int MODE, int NR, int KSL, int D>
 __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restrict__ ws) {
     constexpr int NKB = KSL / 128;
@@ -411,7 +417,8 @@ __global__ void __launch_bounds__(256, 1) k_gemv_ml(GemvArgs a, float* __restric
             const int c = ppos ^ r;  // source chunk landing at position ppos of row r
             const uint16_t* src = a.W + row_of(u, j) * K + k0 + kb * 128 + c * 8;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                             (__attribute__((address_space(3))) void*)(ring + slot * SLOT + q * 1024), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(ring + slot * SLOT + q * 1024), 16, 0,
+                                             PGMI_ML_AUX);
         }
     };
     int grp = blockIdx.x * wpb + wave;

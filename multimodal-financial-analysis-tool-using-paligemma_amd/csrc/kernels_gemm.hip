@@ -420,7 +420,7 @@ __device__ __forceinline__ void vm_wait_tiles(int n) {
 // on every XCD (8-image down projection: 718 MB per launch fetched for ≈180 MB of operands).  Inside
 // a block the row tiles of one weight panel stay adjacent.
 __device__ __forceinline__ void xcd_tile(int n_mt_x, int& mt, int& nt, int& z) {
-    const int n_mt = n_mt_x & 1023, xb = n_mt_x >> 10;
+    const int n_mt = n_mt_x & 1023, xb = (n_mt_x >> 10) & 0xFFFFF;  // (bit 30: k_gemm_w's weight policy)
     const int S = gridDim.y;
     const int G = gridDim.x * S;
     const int lin = blockIdx.x + blockIdx.y * gridDim.x;
@@ -689,14 +689,26 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
             src[i] = base + (long)row * ld + gk[i];
         }
         const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+        // one row tile (n_mt == 1, flagged in bit 30 of n_mt by launch_w): every weight byte is read by one
+        // workgroup once, so those pieces stream non-temporal; the activation panel, which every workgroup
+        // re-reads, keeps the default policy.  Same box (tools/gpu_r4l.sh, the M = 288 gate|up): 43.1 / 43.8 /
+        // 43.3 -> 41.2 / 41.7 / 41.4 us in situ, 224 px prefill 3.80 -> 3.77-3.79 ms
+        const bool wnt = (n_mt >> 30) & 1;
         auto issue = [&](int kt, int slot) {
             const int kel = kt * 64;
             if (kel + 64 <= K) {
 #pragma unroll
-                for (int i = 0; i < GPW; ++i)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
-                                                     (__attribute__((address_space(3))) void*)(smem_w + slot * SBYTES + loff[i]),
-                                                     16, 0, 0);
+                for (int i = 0; i < GPW; ++i) {
+                    const int p = lw + LW * i < PCS ? lw + LW * i : lw + LW * i - PCS;
+                    if (wnt && p >= APC)
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
+                                                         (__attribute__((address_space(3))) void*)(smem_w + slot * SBYTES + loff[i]),
+                                                         16, 0, 2);
+                    else
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
+                                                         (__attribute__((address_space(3))) void*)(smem_w + slot * SBYTES + loff[i]),
+                                                         16, 0, 0);
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < GPW; ++i) {
@@ -1386,7 +1398,8 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
     dim3 grid(n_mt * n_nt, split);
-    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10);
+    static const bool wnt_off = [] { const char* e = getenv("PGMI_GEMM_WNT"); return e && atoi(e) == 0; }();
+    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10) | (n_mt == 1 && !wnt_off ? 1 << 30 : 0);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>),

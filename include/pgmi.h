@@ -157,6 +157,11 @@ int pgmi_decode_embeds_dev(pgmi_ctx* ctx, const void* embeds, int B, void* kv, i
  * called again with identical pointer and size arguments (the graph is captured on the second
  * such call; a replay reads the same addresses as the eager call would).  0 = always eager. */
 int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
+/* Batched decode (B >= 3, MFMA projections) RMSNorm form: 0 = each input norm computed once per row
+ * and read unstaged by the q|k|v / gate|up projections (default), 1 = staged inside each projection,
+ * -1 = back to the default (PGMI_MF_STAGED env).  Same arithmetic either way (bf16 normalised rows);
+ * drops captured decode graphs.  A tuning / test switch, no reference counterpart. */
+int pgmi_set_decode_staged_norm(pgmi_ctx* ctx, int on);
 /* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden
  * rows: logits (device fp32 [rows][vocab]) = fp32(bf16(normed . E^T)) with the tied embedding E.
  * Together with pgmi_lm_final_hidden this materialises the prefill's all-row logits on demand

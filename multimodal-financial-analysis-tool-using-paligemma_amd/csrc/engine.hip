@@ -120,6 +120,7 @@ struct pgmi_ctx {
     // identical pointer/shape arguments (a replay is the eager call: kernels read the same
     // addresses at run time), captured on the second such call
     bool prefill_graph = true;
+    int mf_staged = -1;  // batched decode RMSNorm form (mf_staged()); -1 = PGMI_MF_STAGED / default
     // device step state as the last enqueued per-phase decode step leaves it (advanced in-graph)
     bool step_known = false;
     int step_kv = 0, step_pos = 0;
@@ -924,12 +925,13 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
-// The batched form's RMSNorms: staged by each projection itself (default) or computed once per row
-// (k_rows_norm / the combine's fused norm) and read unstaged -- measured equal (B = 8 step 1.5449 vs
-// 1.5452 ms, same box), so the form with fewer launches stays; PGMI_MF_STAGED=0 selects the other
-static bool mf_staged() {
-    static const bool v = [] { const char* e = getenv("PGMI_MF_STAGED"); return !e || atoi(e) != 0; }();
-    return v;
+// The batched form's RMSNorms: computed once per row (k_rows_norm / the down combine's fused norm) and read
+// unstaged by q|k|v and gate|up (default), or staged by each projection itself (PGMI_MF_STAGED=1).  Equal
+// while the weight streams were non-temporal (B = 8 step 1.5449 vs 1.5452 ms); with the default cache policy
+// (kernels_gemv_mfma.hip PGMI_MF_NT) the unstaged form wins, same box: 1.4523 / 1.4550 -> 1.4330 / 1.4320 ms
+static bool mf_staged(const pgmi_ctx* x) {
+    static const bool env = [] { const char* e = getenv("PGMI_MF_STAGED"); return e && atoi(e) != 0; }();
+    return x->mf_staged < 0 ? env : x->mf_staged != 0;
 }
 
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
@@ -951,7 +953,7 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     // B >= 3 (MFMA projections): every RMSNorm is computed once per row (k_rows_norm after o_proj, fused
     // into the down projection's combine for the next layer's input norm) and the q|k|v and gate|up
     // projections read the normalised rows dHn without staging
-    const bool mf = B >= gemv_mf_min_batch() && !mf_staged();
+    const bool mf = B >= gemv_mf_min_batch() && !mf_staged(x);
     if (mf && c.t_layers > 0) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
@@ -1026,6 +1028,15 @@ int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
         us[i] = a * 1e3f;
         us[L + i] = b * 1e3f;
     }
+    return 0;
+}
+
+int pgmi_set_decode_staged_norm(pgmi_ctx* x, int on) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    x->mf_staged = on < 0 ? -1 : on != 0;
+    for (auto& kv : x->graphs)  // captured steps hold the other form's launches
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    x->graphs.clear();
     return 0;
 }
 

@@ -56,9 +56,19 @@ def _inputs(G, B):
     return ids, px
 
 
-@pytest.mark.parametrize("B", [3, 5, 8])
+# staged = 1: the batched decode's per-projection staged RMSNorm form (pgmi_set_decode_staged_norm),
+# the non-default of the two; same fixtures, same bars
+@pytest.mark.parametrize("B,staged", [(3, 0), (5, 0), (8, 0), (8, 1)])
 @torch.no_grad()
-def test_batch_rows_teacher_forced_vs_own_reference(eng, G, F, B):
+def test_batch_rows_teacher_forced_vs_own_reference(eng, G, F, B, staged):
+    eng.set_decode_staged_norm(staged)
+    try:
+        _teacher_forced_rows(eng, G, F, B, "staged" if staged else "")
+    finally:
+        eng.set_decode_staged_norm(-1)
+
+
+def _teacher_forced_rows(eng, G, F, B, tag):
     ids, px = _inputs(G, B)
     L = ids.shape[1]
     kv = eng.new_kv(B, 384)
@@ -80,7 +90,7 @@ def test_batch_rows_teacher_forced_vs_own_reference(eng, G, F, B):
         decisive = G["margin"][b] > 0.25
         assert np.array_equal(am[decisive], ref_toks[b][decisive]), (b, am, ref_toks[b])
         s = ours[b][:, sidx].cpu().numpy()
-        check_model_parity(f"batch{B}/row{b}", s, G["sample_vals"][b], F["sample_vals"][b])
+        check_model_parity(f"batch{B}{tag}/row{b}", s, G["sample_vals"][b], F["sample_vals"][b])
 
 
 @pytest.mark.parametrize("B", [3, 8])

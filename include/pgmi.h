@@ -162,6 +162,13 @@ int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
  * -1 = back to the default (PGMI_MF_STAGED env).  Same arithmetic either way (bf16 normalised rows);
  * drops captured decode graphs.  A tuning / test switch, no reference counterpart. */
 int pgmi_set_decode_staged_norm(pgmi_ctx* ctx, int on);
+/* SigLIP LayerNorm fold at the one-image plan: 1 = out_proj / fc2 reduce their split-K
+ * partials in the GEMM with the next LayerNorm's row statistics, and q|k|v / fc1 apply that LayerNorm
+ * in their epilogue through weights folded at pgmi_prepare (bf16(W diag(gamma)), fp32 column terms);
+ * 0 (default: measured faster) = the separate split-K reduction + LayerNorm launches; -1 = default
+ * (PGMI_VISION_LNFOLD env).
+ * Drops captured prefill graphs.  A tuning / test switch, no reference counterpart. */
+int pgmi_set_vision_lnfold(pgmi_ctx* ctx, int on);
 /* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden
  * rows: logits (device fp32 [rows][vocab]) = fp32(bf16(normed . E^T)) with the tied embedding E.
  * Together with pgmi_lm_final_hidden this materialises the prefill's all-row logits on demand

@@ -97,6 +97,13 @@ struct pgmi_ctx {
     int64_t* dids_tmp;
     // vision workspace (rows = max_batch*N)
     uint16_t *vX, *vT, *vQKV, *vAO, *vH, *vP;
+    // SigLIP LayerNorms folded into q|k|v and fc1 (one-image plan, vision_lnfold): per layer the folded
+    // weights bf16(W diag(gamma)) and (c1, c0); the residual projections' row statistics and counters
+    uint16_t *vWqkv_f = nullptr, *vWfc1_f = nullptr;
+    float *vCqkv = nullptr, *vCfc1 = nullptr;  // [layer][2][N]: c1 then c0
+    float *vLnSt = nullptr, *vLnMr = nullptr;
+    unsigned *vTcnt = nullptr, *vRcnt = nullptr;
+    int vision_lnfold = -1;  // -1: PGMI_VISION_LNFOLD (default off: measured slower)
     float* ws;
     size_t ws_bytes;
     // decode workspace
@@ -588,6 +595,19 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->vAO, RV * c.v_hidden))) return rc;
         if ((rc = dalloc_t(x, &x->vH, RV * c.v_intermediate))) return rc;
         if ((rc = dalloc_t(x, &x->vP, RV * x->kpad))) return rc;
+        {
+            const size_t D = c.v_hidden, Iv = c.v_intermediate, Lv = c.v_layers;
+            if ((rc = dalloc_t(x, &x->vWqkv_f, Lv * 3 * D * D))) return rc;
+            if ((rc = dalloc_t(x, &x->vWfc1_f, Lv * Iv * D))) return rc;
+            if ((rc = dalloc_t(x, &x->vCqkv, Lv * 2 * 3 * D))) return rc;
+            if ((rc = dalloc_t(x, &x->vCfc1, Lv * 2 * Iv))) return rc;
+            if ((rc = dalloc_t(x, &x->vLnSt, (size_t)N * kResLnSegs * 2))) return rc;
+            if ((rc = dalloc_t(x, &x->vLnMr, (size_t)N * 2))) return rc;
+            if ((rc = dalloc_t(x, &x->vTcnt, (size_t)kResLnTiles))) return rc;
+            if ((rc = dalloc_t(x, &x->vRcnt, (size_t)kResLnRowTiles))) return rc;
+            HIPCHK(hipMemset(x->vTcnt, 0, kResLnTiles * sizeof(unsigned)));
+            HIPCHK(hipMemset(x->vRcnt, 0, kResLnRowTiles * sizeof(unsigned)));
+        }
         x->ws_bytes = (size_t)64 << 20;
         if ((rc = dalloc(x, reinterpret_cast<void**>(&x->ws), x->ws_bytes))) return rc;
         const int B = c.max_batch;
@@ -620,6 +640,15 @@ int pgmi_prepare(pgmi_ctx* x) {
     // derived tensors
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
+    for (int i = 0; i < c.v_layers; ++i) {  // vision_lnfold's folded projections (rebuilt with the weights)
+        const long D = c.v_hidden, Iv = c.v_intermediate;
+        ln_fold_weights(nullptr, VL(x, i, "self_attn.q_proj.weight"), VL(x, i, "layer_norm1.weight"),
+                        VL(x, i, "layer_norm1.bias"), VL(x, i, "self_attn.q_proj.bias"), (int)(3 * D), (int)D,
+                        x->vWqkv_f + i * 3 * D * D, x->vCqkv + i * 6 * D, x->vCqkv + i * 6 * D + 3 * D);
+        ln_fold_weights(nullptr, VL(x, i, "mlp.fc1.weight"), VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
+                        VL(x, i, "mlp.fc1.bias"), (int)Iv, (int)D, x->vWfc1_f + i * Iv * D, x->vCfc1 + i * 2 * Iv,
+                        x->vCfc1 + i * 2 * Iv + Iv);
+    }
     LAUNCHCHK();
     std::vector<uint16_t> cs, sn;
     if (!x->host_cos.empty()) {
@@ -693,6 +722,37 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
     return 0;
 }
 
+// SigLIP LayerNorm fold (round 4): at the one-image plan the residual projections (out_proj, fc2) reduce
+// their split-K partials in the GEMM's last-arriving workgroup per tile and leave each row's LayerNorm
+// (mean, rstd); q|k|v and fc1 read the raw residual rows and apply the LayerNorm in their epilogue
+// through folded weights (kernels_gemm.hip gemm_res_ln / gemm_lnfold): two launches fewer per layer.
+// Measured slower, off by default (PGMI_VISION_LNFOLD=1 or pgmi_set_vision_lnfold(ctx, 1) turns it on;
+// profiles/r04_vision_lnfold_ab.txt): the two in-launch hand-offs per residual projection (write-through
+// partials -> tile arrival -> coherent reads; segment statistics -> row-tile arrival) cost more than the
+// launch boundary they replace: out_proj 5.8 + 5.1 (reduction + LayerNorm) -> 16.8-18.5 us, fc2 12.3-13.6
+// + 5.8 -> 26.5-29.1 us, tower 1.51 -> 1.95-1.99 ms.  Shapes whose plans have no such form (448 px,
+// batched images) always keep splitk_res_norm.
+static void res_ln_args(pgmi_ctx* x, EpiArgs& e, float eps) {
+    e.tcnt = x->vTcnt;
+    e.rcnt = x->vRcnt;
+    e.lnst = x->vLnSt;
+    e.lnmr = x->vLnMr;
+    e.ln_eps = eps;
+}
+
+static bool vision_lnfold(pgmi_ctx* x, int rows) {
+    static const bool env = [] { const char* e = getenv("PGMI_VISION_LNFOLD"); return e && atoi(e) != 0; }();
+    const bool on = x->vision_lnfold < 0 ? env : x->vision_lnfold != 0;
+    const pgmi_config& c = x->c;
+    if (!on || rows != n_img(c) || c.v_layers < 2) return false;
+    const int D = c.v_hidden, Iv = c.v_intermediate;
+    EpiArgs e{};
+    return gemm_lnfold(nullptr, nullptr, D, nullptr, rows, 3 * D, D, false, e, true) &&
+           gemm_lnfold(nullptr, nullptr, D, nullptr, rows, Iv, D, true, e, true) &&
+           gemm_res_ln(nullptr, nullptr, D, nullptr, rows, D, D, e, x->ws, x->ws_bytes, true) > 0 &&
+           gemm_res_ln(nullptr, nullptr, Iv, nullptr, rows, D, Iv, e, x->ws, x->ws_bytes, true) > 0;
+}
+
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats) {
     const pgmi_config& c = x->c;
     const int N = n_img(c), D = c.v_hidden, Iv = c.v_intermediate, rows = B * N;
@@ -708,14 +768,24 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
     gemm(s, x->vP, x->kpad, x->patch_w, x->kpad, rows, D, x->kpad, EPI_BIAS_POS, e, x->ws, x->ws_bytes);
     const float scale = (float)std::pow((double)(D / c.v_heads), -0.5);  // head_dim**-0.5 (:89)
     // LayerNorm1 of layer 0; every later LayerNorm is fused with the preceding projection's
-    // split-K reduction + bias + residual (splitk_res_norm)
+    // split-K reduction + bias + residual (splitk_res_norm), or, under vision_lnfold, computed as row
+    // statistics by that projection (gemm_res_ln) and applied by the next one (gemm_lnfold)
     layernorm(s, x->vX, VL(x, 0, "layer_norm1.weight"), VL(x, 0, "layer_norm1.bias"), eps, x->vT, rows, D);
+    const bool fold = vision_lnfold(x, rows);
     for (int i = 0; i < c.v_layers; ++i) {
+        const bool last = i + 1 == c.v_layers;
         EpiArgs q{};
         q.bias = VL(x, i, "self_attn.q_proj.bias");  // q|k|v biases adjacent
         q.out = x->vQKV;
         q.ldo = 3 * D;
-        gemm(s, x->vT, D, VL(x, i, "self_attn.q_proj.weight"), D, rows, 3 * D, D, EPI_BIAS, q, x->ws, x->ws_bytes);
+        if (fold && i > 0) {
+            q.lnmr = x->vLnMr;
+            q.lnc1 = x->vCqkv + (long)i * 6 * D;
+            q.lnc0 = q.lnc1 + 3 * D;
+            gemm_lnfold(s, x->vX, D, x->vWqkv_f + (long)i * 3 * D * D, rows, 3 * D, D, false, q);
+        } else {
+            gemm(s, x->vT, D, VL(x, i, "self_attn.q_proj.weight"), D, rows, 3 * D, D, EPI_BIAS, q, x->ws, x->ws_bytes);
+        }
         AttnArgs a{};
         a.q = x->vQKV; a.q_b_stride = (long)N * 3 * D; a.q_row_stride = 3 * D; a.q_head_stride = 72;
         a.k = x->vQKV + D; a.k_b_stride = a.q_b_stride; a.k_row_stride = 3 * D; a.k_head_stride = 72;
@@ -727,18 +797,34 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
         EpiArgs o{};
         o.bias = VL(x, i, "self_attn.out_proj.bias");
         o.res = x->vX; o.ldr = D; o.out = x->vX; o.ldo = D;
-        int sp = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
-                      x->ws_bytes, 0, true);
-        splitk_res_norm(s, x->ws, sp, o.bias, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"), eps,
-                        x->vT, rows, D);
+        if (fold) {
+            res_ln_args(x, o, eps);
+            gemm_res_ln(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), rows, D, D, o, x->ws, x->ws_bytes);
+        } else {
+            int sp = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
+                          x->ws_bytes, 0, true);
+            splitk_res_norm(s, x->ws, sp, o.bias, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
+                            eps, x->vT, rows, D);
+        }
         EpiArgs f1{};
         f1.bias = VL(x, i, "mlp.fc1.bias"); f1.out = x->vH; f1.ldo = Iv;
-        gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
+        if (fold) {
+            f1.lnmr = x->vLnMr;
+            f1.lnc1 = x->vCfc1 + (long)i * 2 * Iv;
+            f1.lnc0 = f1.lnc1 + Iv;
+            gemm_lnfold(s, x->vX, D, x->vWfc1_f + (long)i * Iv * D, rows, Iv, D, true, f1);
+        } else {
+            gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
+        }
         EpiArgs f2{};
         f2.bias = VL(x, i, "mlp.fc2.bias"); f2.res = x->vX; f2.ldr = D; f2.out = x->vX; f2.ldo = D;
-        sp = gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws, x->ws_bytes, 0,
-                  true);
-        const bool last = i + 1 == c.v_layers;
+        if (fold && !last) {
+            res_ln_args(x, f2, eps);
+            gemm_res_ln(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), rows, D, Iv, f2, x->ws, x->ws_bytes);
+            continue;
+        }
+        const int sp = gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws,
+                            x->ws_bytes, 0, true);
         splitk_res_norm(s, x->ws, sp, f2.bias, x->vX,
                         last ? W(x, "vision_tower.vision_model.post_layernorm.weight") : VL(x, i + 1, "layer_norm1.weight"),
                         last ? W(x, "vision_tower.vision_model.post_layernorm.bias") : VL(x, i + 1, "layer_norm1.bias"),
@@ -1028,6 +1114,13 @@ int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
         us[i] = a * 1e3f;
         us[L + i] = b * 1e3f;
     }
+    return 0;
+}
+
+int pgmi_set_vision_lnfold(pgmi_ctx* x, int on) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    x->vision_lnfold = on < 0 ? -1 : on != 0;
+    clear_pgraphs(x);  // captured towers hold the other form's launches
     return 0;
 }
 

@@ -17,6 +17,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "coh.h"
 #include "common.h"
 #include "launch.h"
 
@@ -44,6 +45,12 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float
             break;
         case EPI_F32: ea.out_f32[(long)m * ea.ldo + n] = rbf(acc); break;
         case EPI_GEGLU: ea.out[(long)m * ea.ldo + n] = f2bf(rbf(gelu_tanh(rbf(acc))) * rbf(acc2)); break;
+        case EPI_LNB:
+        case EPI_LNB_GELU: {
+            const float o = ea.lnmr[2 * m + 1] * (acc - ea.lnmr[2 * m] * ea.lnc1[n]) + ea.lnc0[n];
+            ea.out[(long)m * ea.ldo + n] = f2bf(EPI == EPI_LNB ? o : gelu_tanh(rbf(o)));
+            break;
+        }
     }
 }
 
@@ -66,8 +73,11 @@ template <int EPI, int TM, int TN>
 struct EpiOps {
     static constexpr bool HB = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_POS;
     static constexpr bool HX = EPI == EPI_BIAS_RES || EPI == EPI_RES || EPI == EPI_BIAS_POS;
+    static constexpr bool HL = EPI == EPI_LNB || EPI == EPI_LNB_GELU;
     float bv[HB ? TN : 1];
     float xv[HX ? TM : 1][HX ? TN : 1][4];
+    float c0[HL ? TN : 1], c1[HL ? TN : 1];         // LayerNorm fold: per column
+    float mu[HL ? TM : 1][4], rs[HL ? TM : 1][4];  // per row
 };
 
 template <int EPI, int TM, int TN>
@@ -80,6 +90,22 @@ __device__ __forceinline__ void epi_load(const EpiArgs& ea, int M, int N, int mb
         const int n = nb + j * 16 + (lane & 15);
         ncl[j] = n < N ? n : N - 1;
         if constexpr (E::HB) e.bv[j] = bf2f(ea.bias[ncl[j]]);
+        if constexpr (E::HL) {
+            e.c0[j] = ea.lnc0[ncl[j]];
+            e.c1[j] = ea.lnc1[ncl[j]];
+        }
+    }
+    if constexpr (E::HL) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = mb + i * 16 + (lane >> 4) * 4 + r;
+                m = m < M ? m : M - 1;
+                const float2 v = *reinterpret_cast<const float2*>(ea.lnmr + 2 * (long)m);
+                e.mu[i][r] = v.x;
+                e.rs[i][r] = v.y;
+            }
     }
     if constexpr (E::HX) {
 #pragma unroll
@@ -117,6 +143,14 @@ __device__ __forceinline__ void epi_apply(const EpiArgs& ea, int M, int N, int m
 #pragma unroll
                 for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(e.xv[i][j][r]));
     }
+    if constexpr (E::HL) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(e.c0[j]), "+v"(e.c1[j]));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(e.mu[i][r]), "+v"(e.rs[i][r]));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -134,6 +168,9 @@ __device__ __forceinline__ void epi_apply(const EpiArgs& ea, int M, int N, int m
                 else if constexpr (EPI == EPI_RES) o = rbf(a) + e.xv[i][j][r];
                 else if constexpr (EPI == EPI_BIAS_POS) o = rbf(a + e.bv[j]) + e.xv[i][j][r];
                 else if constexpr (EPI == EPI_GEGLU) o = rbf(gelu_tanh(rbf(a))) * rbf(acc2[i][j][r]);
+                else if constexpr (EPI == EPI_LNB) o = e.rs[i][r] * (a - e.mu[i][r] * e.c1[j]) + e.c0[j];
+                else if constexpr (EPI == EPI_LNB_GELU)
+                    o = gelu_tanh(rbf(e.rs[i][r] * (a - e.mu[i][r] * e.c1[j]) + e.c0[j]));
                 if (m < M && n < N) {
                     if constexpr (EPI == EPI_F32) ea.out_f32[(long)m * ea.ldo + n] = rbf(a);
                     else ea.out[(long)m * ea.ldo + n] = f2bf(o);
@@ -443,6 +480,135 @@ __device__ __forceinline__ void xcd_tile(int n_mt_x, int& mt, int& nt, int& z) {
     nt = idx / (n_mt * S);
 }
 
+// gemm_res_ln's tail of a split-K k_gemm_p workgroup (its fp32 partial already stored write-through).
+// Per output tile the workgroup whose arrival count comes last reduces the S slabs in the fixed order
+// of k_splitk_res_norm (bitwise the same sum), adds bias and residual -> ea.out (bf16), and stores
+// per row and 32-column segment (sum, sum of squared deviations from the segment mean) of the bf16
+// result; per row tile the workgroup that completes the last tile combines the segments (Chan's
+// pairwise form, fixed order) into (mean, rstd) -> ea.lnmr.  Hand-offs per coh.h: write-through
+// stores, each storing wave drained, a barrier, one lane counts; the counting lane of the last
+// arrival resets the counter for the next launch.  S <= kResLnMaxSplit, N / 32 <= kResLnMaxSeg.
+constexpr int kResLnMaxSplit = 4, kResLnMaxSeg = kResLnSegs;
+template <int TM, int TN, int WN, int BM>
+__device__ __forceinline__ void res_ln_tail(const EpiArgs& ea, const float* __restrict__ ws, int M, int N, int mt,
+                                            int nt, int n_nt, int z, int wm, int wn, int lane,
+                                            const f32x4 (&acc)[TM][TN]) {
+    __shared__ int last_tile, last_rows;
+    const int tid = threadIdx.x;
+    const int S = gridDim.y;
+    constexpr int SEGW = TN * 16;
+    const int nseg = N / SEGW;
+    const int m0 = mt * BM + wm * TM * 16, n0 = nt * WN * SEGW + wn * SEGW;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* tc = ea.tcnt + (long)mt * n_nt + nt;
+    if (tid == 0) {
+        const bool l = __hip_atomic_fetch_add(tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)S;
+        if (l) __hip_atomic_store(tc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_tile = l;
+    }
+    __syncthreads();
+    if (!last_tile) return;
+    // every slab's value, the bias and the residual issued before any is used (rows past M clamped)
+    float v[kResLnMaxSplit][TM][TN][4];
+    float bv[TN], xv[TM][TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[j] = bf2f(ea.bias[n0 + j * 16 + (lane & 15)]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+            m = m < M ? m : M - 1;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + j * 16 + (lane & 15);
+                xv[i][j][r] = bf2f(ea.res[(long)m * ea.ldr + n]);
+#pragma unroll
+                for (int q = 0; q < kResLnMaxSplit; ++q)
+                    v[q][i][j][r] = ldf_coh(ws + ((long)(q < S ? q : 0) * M + m) * N + n);
+            }
+        }
+    float x[TM][TN][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float a = z == 0 ? acc[i][j][r] : v[0][i][j][r];
+#pragma unroll
+                for (int q = 1; q < kResLnMaxSplit; ++q) {
+                    const float p = z == q ? acc[i][j][r] : v[q][i][j][r];
+                    a = q < S ? a + p : a;
+                }
+                const uint16_t o = f2bf(rbf(a + bv[j]) + xv[i][j][r]);
+                const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+                if (m < M) ea.out[(long)m * ea.ldo + n0 + j * 16 + (lane & 15)] = o;
+                x[i][j][r] = bf2f(o);
+            }
+    // segment statistics: the 16 lanes of one (lane >> 4) hold the segment's columns of 4 rows
+    const int seg = nt * WN + wn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) sm += x[i][j][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+            const float mean = sm / (float)SEGW;
+            float d2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const float d = x[i][j][r] - mean;
+                d2 += d * d;
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
+            const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+            if ((lane & 15) == 0 && m < M) {
+                stf_coh(ea.lnst + ((long)m * nseg + seg) * 2, sm);
+                stf_coh(ea.lnst + ((long)m * nseg + seg) * 2 + 1, d2);
+            }
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        unsigned* rc = ea.rcnt + mt;
+        const bool l = __hip_atomic_fetch_add(rc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)n_nt;
+        if (l) __hip_atomic_store(rc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_rows = l;
+    }
+    __syncthreads();
+    if (!last_rows || tid >= BM) return;
+    const int m = mt * BM + tid;
+    if (m >= M) return;
+    float sv[kResLnMaxSeg], dv[kResLnMaxSeg];
+#pragma unroll
+    for (int g = 0; g < kResLnMaxSeg; ++g) {
+        const int gc = g < nseg ? g : nseg - 1;
+        const unsigned long long w = __hip_atomic_load(
+            reinterpret_cast<const unsigned long long*>(ea.lnst + ((long)m * nseg + gc) * 2), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        sv[g] = __uint_as_float((unsigned)w);
+        dv[g] = __uint_as_float((unsigned)(w >> 32));
+    }
+    float tot = 0.f;
+#pragma unroll
+    for (int g = 0; g < kResLnMaxSeg; ++g) tot = g < nseg ? tot + sv[g] : tot;
+    const float mean = tot / (float)N;
+    float m2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < kResLnMaxSeg; ++g) {
+        const float dm = sv[g] / (float)SEGW - mean;
+        m2 = g < nseg ? m2 + (dv[g] + (float)SEGW * dm * dm) : m2;
+    }
+    ea.lnmr[2 * (long)m] = mean;
+    ea.lnmr[2 * (long)m + 1] = 1.0f / sqrtf(m2 / (float)N + ea.ln_eps);
+}
+
 template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
@@ -605,6 +771,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 
     // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r
     if constexpr (SPLIT) {
+        const bool fused = ea.tcnt != nullptr;  // gemm_res_ln: partials write-through, reduced below
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -613,9 +780,14 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
+                    if (m < M && n < N) {
+                        if (fused) stf_coh(ws + ((long)z * M + m) * N + n, acc[0][i][j][r]);
+                        else ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
+                    }
                 }
             }
+        if constexpr (NB == 1 && EPI == EPI_BIAS_RES)
+            if (fused) res_ln_tail<TM, TN, WN, BM>(ea, ws, M, N, mt, nt, n_nt, z, wm, wn, lane, acc[0]);
     } else if constexpr (EPI == EPI_ROPE) {
         rope_apply<TM>(ea, M, epi_mb, lane, rope_ops, acc[0]);
     } else {
@@ -1587,6 +1759,63 @@ bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W,
     }
 #undef P_
 #undef W_
+    return true;
+}
+
+// gemm_res_ln launcher: the split-K k_gemm_p with the fused tail (no k_splitk_epi after it)
+template <int WM, int TM, int TN, int ST>
+static int launch_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
+                         const EpiArgs& ea, float* ws, int split, bool dry) {
+    constexpr int NW = 4, WN = NW / WM, BM = WM * TM * 16, BN = WN * TN * 16;
+    constexpr int STQ = (size_t)ST * (BM + BN) * 128 <= 163840 ? ST : ST - 1;
+    constexpr size_t lds = (size_t)STQ * (BM + BN) * 128;
+    const int n_mt = (M + BM - 1) / BM, n_nt = N / BN;
+    if (N % BN != 0 || N / (TN * 16) > kResLnMaxSeg || n_mt * n_nt > kResLnTiles || n_mt > kResLnRowTiles) return 0;
+    if (dry) return split;
+    const int nkt = (K + 63) / 64, per = (nkt + split - 1) / split;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, 1, STQ, EPI_BIAS_RES, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, BN, K) << 10);
+    PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, 1, STQ, EPI_BIAS_RES, true>), dim3(n_mt * n_nt, split), dim3(64 * NW), lds,
+                     s, A, lda, W, K, M, N, K, per, ea, ws, 0L, nmx, n_nt);
+    return split;
+}
+
+int gemm_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K, const EpiArgs& ea,
+                float* ws, size_t ws_bytes, bool dry) {
+    const Plan p = choose(M, N, K, false);
+    const int nkt = (K + 63) / 64;
+    const int per = (nkt + p.split - 1) / p.split;
+    const int split = (nkt + per - 1) / per;  // every K range non-empty (as gemm)
+    if (split < 2 || split > kResLnMaxSplit || (size_t)split * M * N * sizeof(float) > ws_bytes) return 0;
+    if (!dry && (!ea.tcnt || !ea.rcnt || !ea.lnst || !ea.lnmr || !ea.bias || !ea.res || !ea.out)) return 0;
+    switch (p.cfg) {
+        case P64x64s4: return launch_res_ln<2, 2, 2, 4>(s, A, lda, W, M, N, K, ea, ws, split, dry);
+        case P96x64s4: return launch_res_ln<2, 3, 2, 4>(s, A, lda, W, M, N, K, ea, ws, split, dry);
+        default: return 0;
+    }
+}
+
+bool gemm_lnfold(hipStream_t s, const uint16_t* A, int lda, const uint16_t* Wf, int M, int N, int K, bool gelu,
+                 const EpiArgs& ea, bool dry) {
+    const Plan p = choose(M, N, K, false);
+    if (p.split != 1) return false;
+#define F_(wm, tm, tn, st)                                                                                       \
+    do {                                                                                                         \
+        if (dry) break;                                                                                          \
+        if (gelu) launch_p<4, wm, tm, tn, st, EPI_LNB_GELU>(s, A, lda, Wf, K, M, N, K, ea, nullptr, 1, 0);       \
+        else launch_p<4, wm, tm, tn, st, EPI_LNB>(s, A, lda, Wf, K, M, N, K, ea, nullptr, 1, 0);                 \
+    } while (0)
+    switch (p.cfg) {
+        case P64x64s4: F_(2, 2, 2, 4); break;
+        case P96x64s4: F_(2, 3, 2, 4); break;
+        default: return false;
+    }
+#undef F_
     return true;
 }
 

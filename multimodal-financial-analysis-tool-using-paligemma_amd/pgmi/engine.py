@@ -340,6 +340,10 @@ class Engine:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
 
+    def set_vision_lnfold(self, on: int) -> None:
+        """SigLIP LayerNorm fold (one image): 1 on, 0 separate LayerNorm launches (default), -1 default."""
+        N.check(self.lib.pgmi_set_vision_lnfold(self.ctx, int(on)), "pgmi_set_vision_lnfold")
+
     def set_decode_staged_norm(self, on: int) -> None:
         """Batched decode RMSNorm form: 0 once per row (default), 1 staged per projection, -1 default."""
         N.check(self.lib.pgmi_set_decode_staged_norm(self.ctx, int(on)), "pgmi_set_decode_staged_norm")

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4: SigLIP LayerNorm fold (one-image tower) -- parity tests, then tower time fold on / off.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out
+mkdir -p $O
+cd $R
+PGMI_PARITY_LOG=$O/parity_fold.jsonl timeout -k 10 600 python -u -m pytest tests/test_gpu_full.py -x -q \
+  -k "lnfold or teacher_forced_64 or prefill_448 or no_kv" --timeout 300 --timeout-method thread > $O/t_fold.log 2>&1
+for i in 1 2; do
+  for v in 1 0; do
+    PGMI_VISION_LNFOLD=$v timeout -k 10 300 python bench.py --batch 1 --steps 16 --warmup 4 --no-448 --no-extra --no-api \
+      --no-cpu-baseline --prefill-iters 30 > $O/vf.log 2>&1
+    echo "lnfold=$v $(tail -n 1 $O/vf.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["prefill_vision_ms"], d["prefill_ms"], d["value"])')" >> $O/ab_r4n.txt
+  done
+done

@@ -104,6 +104,7 @@ struct pgmi_ctx {
     float *vLnSt = nullptr, *vLnMr = nullptr;
     unsigned *vTcnt = nullptr, *vRcnt = nullptr;
     int vision_lnfold = -1;  // -1: PGMI_VISION_LNFOLD (default off: measured slower)
+    bool vfold_ready = false;
     float* ws;
     size_t ws_bytes;
     // decode workspace
@@ -595,19 +596,6 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->vAO, RV * c.v_hidden))) return rc;
         if ((rc = dalloc_t(x, &x->vH, RV * c.v_intermediate))) return rc;
         if ((rc = dalloc_t(x, &x->vP, RV * x->kpad))) return rc;
-        {
-            const size_t D = c.v_hidden, Iv = c.v_intermediate, Lv = c.v_layers;
-            if ((rc = dalloc_t(x, &x->vWqkv_f, Lv * 3 * D * D))) return rc;
-            if ((rc = dalloc_t(x, &x->vWfc1_f, Lv * Iv * D))) return rc;
-            if ((rc = dalloc_t(x, &x->vCqkv, Lv * 2 * 3 * D))) return rc;
-            if ((rc = dalloc_t(x, &x->vCfc1, Lv * 2 * Iv))) return rc;
-            if ((rc = dalloc_t(x, &x->vLnSt, (size_t)N * kResLnSegs * 2))) return rc;
-            if ((rc = dalloc_t(x, &x->vLnMr, (size_t)N * 2))) return rc;
-            if ((rc = dalloc_t(x, &x->vTcnt, (size_t)kResLnTiles))) return rc;
-            if ((rc = dalloc_t(x, &x->vRcnt, (size_t)kResLnRowTiles))) return rc;
-            HIPCHK(hipMemset(x->vTcnt, 0, kResLnTiles * sizeof(unsigned)));
-            HIPCHK(hipMemset(x->vRcnt, 0, kResLnRowTiles * sizeof(unsigned)));
-        }
         x->ws_bytes = (size_t)64 << 20;
         if ((rc = dalloc(x, reinterpret_cast<void**>(&x->ws), x->ws_bytes))) return rc;
         const int B = c.max_batch;
@@ -640,15 +628,7 @@ int pgmi_prepare(pgmi_ctx* x) {
     // derived tensors
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
-    for (int i = 0; i < c.v_layers; ++i) {  // vision_lnfold's folded projections (rebuilt with the weights)
-        const long D = c.v_hidden, Iv = c.v_intermediate;
-        ln_fold_weights(nullptr, VL(x, i, "self_attn.q_proj.weight"), VL(x, i, "layer_norm1.weight"),
-                        VL(x, i, "layer_norm1.bias"), VL(x, i, "self_attn.q_proj.bias"), (int)(3 * D), (int)D,
-                        x->vWqkv_f + i * 3 * D * D, x->vCqkv + i * 6 * D, x->vCqkv + i * 6 * D + 3 * D);
-        ln_fold_weights(nullptr, VL(x, i, "mlp.fc1.weight"), VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
-                        VL(x, i, "mlp.fc1.bias"), (int)Iv, (int)D, x->vWfc1_f + i * Iv * D, x->vCfc1 + i * 2 * Iv,
-                        x->vCfc1 + i * 2 * Iv + Iv);
-    }
+    x->vfold_ready = false;  // vision_lnfold's folded projections: rebuilt from these weights on first use
     LAUNCHCHK();
     std::vector<uint16_t> cs, sn;
     if (!x->host_cos.empty()) {
@@ -707,6 +687,8 @@ static int run_graphed(pgmi_ctx* x, hipStream_t s, const std::vector<intptr_t>& 
 }  // extern "C++"
 
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats);
+static bool vision_lnfold(pgmi_ctx* x, int rows);
+static int ensure_vision_fold(pgmi_ctx* x);
 
 int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, void* stream) {
     int rc;
@@ -714,6 +696,7 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
     const pgmi_config& c = x->c;
     if (B < 1 || B > c.max_batch) return fail(PGMI_E_ARG, "batch exceeds max_batch");
     if (!pixels || !feats) return fail(PGMI_E_ARG, "null argument");
+    if (vision_lnfold(x, B * n_img(c)) && (rc = ensure_vision_fold(x))) return rc;
     const std::vector<intptr_t> key{1, (intptr_t)pixels, dtype, B, (intptr_t)feats};
     rc = run_graphed(x, (hipStream_t)stream, key,
                      [&](hipStream_t st) { return vision_body(x, st, pixels, dtype, B, feats); });
@@ -732,6 +715,39 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
 // launch boundary they replace: out_proj 5.8 + 5.1 (reduction + LayerNorm) -> 16.8-18.5 us, fc2 12.3-13.6
 // + 5.8 -> 26.5-29.1 us, tower 1.51 -> 1.95-1.99 ms.  Shapes whose plans have no such form (448 px,
 // batched images) always keep splitk_res_norm.
+// the fold's buffers and folded weights, built on first use after each pgmi_prepare (outside any capture:
+// pgmi_vision calls it before run_graphed)
+static int ensure_vision_fold(pgmi_ctx* x) {
+    if (x->vfold_ready) return 0;
+    const pgmi_config& c = x->c;
+    const size_t D = c.v_hidden, Iv = c.v_intermediate, Lv = c.v_layers, N = n_img(c);
+    int rc;
+    if (!x->vWqkv_f) {
+        if ((rc = dalloc_t(x, &x->vWqkv_f, Lv * 3 * D * D))) return rc;
+        if ((rc = dalloc_t(x, &x->vWfc1_f, Lv * Iv * D))) return rc;
+        if ((rc = dalloc_t(x, &x->vCqkv, Lv * 2 * 3 * D))) return rc;
+        if ((rc = dalloc_t(x, &x->vCfc1, Lv * 2 * Iv))) return rc;
+        if ((rc = dalloc_t(x, &x->vLnSt, N * kResLnSegs * 2))) return rc;
+        if ((rc = dalloc_t(x, &x->vLnMr, N * 2))) return rc;
+        if ((rc = dalloc_t(x, &x->vTcnt, (size_t)kResLnTiles))) return rc;
+        if ((rc = dalloc_t(x, &x->vRcnt, (size_t)kResLnRowTiles))) return rc;
+        HIPCHK(hipMemset(x->vTcnt, 0, kResLnTiles * sizeof(unsigned)));
+        HIPCHK(hipMemset(x->vRcnt, 0, kResLnRowTiles * sizeof(unsigned)));
+    }
+    for (int i = 0; i < c.v_layers; ++i) {
+        ln_fold_weights(nullptr, VL(x, i, "self_attn.q_proj.weight"), VL(x, i, "layer_norm1.weight"),
+                        VL(x, i, "layer_norm1.bias"), VL(x, i, "self_attn.q_proj.bias"), (int)(3 * D), (int)D,
+                        x->vWqkv_f + i * 3 * D * D, x->vCqkv + i * 6 * D, x->vCqkv + i * 6 * D + 3 * D);
+        ln_fold_weights(nullptr, VL(x, i, "mlp.fc1.weight"), VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
+                        VL(x, i, "mlp.fc1.bias"), (int)Iv, (int)D, x->vWfc1_f + i * Iv * D, x->vCfc1 + i * 2 * Iv,
+                        x->vCfc1 + i * 2 * Iv + Iv);
+    }
+    LAUNCHCHK();
+    HIPCHK(hipDeviceSynchronize());
+    x->vfold_ready = true;
+    return 0;
+}
+
 static void res_ln_args(pgmi_ctx* x, EpiArgs& e, float eps) {
     e.tcnt = x->vTcnt;
     e.rcnt = x->vRcnt;
@@ -771,7 +787,7 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
     // split-K reduction + bias + residual (splitk_res_norm), or, under vision_lnfold, computed as row
     // statistics by that projection (gemm_res_ln) and applied by the next one (gemm_lnfold)
     layernorm(s, x->vX, VL(x, 0, "layer_norm1.weight"), VL(x, 0, "layer_norm1.bias"), eps, x->vT, rows, D);
-    const bool fold = vision_lnfold(x, rows);
+    const bool fold = x->vfold_ready && vision_lnfold(x, rows);
     for (int i = 0; i < c.v_layers; ++i) {
         const bool last = i + 1 == c.v_layers;
         EpiArgs q{};

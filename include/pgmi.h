@@ -165,8 +165,9 @@ int pgmi_set_decode_staged_norm(pgmi_ctx* ctx, int on);
 /* SigLIP LayerNorm fold at the one-image plan: 1 = out_proj / fc2 reduce their split-K
  * partials in the GEMM with the next LayerNorm's row statistics, and q|k|v / fc1 apply that LayerNorm
  * in their epilogue through weights folded at pgmi_prepare (bf16(W diag(gamma)), fp32 column terms);
- * 0 (default: measured faster) = the separate split-K reduction + LayerNorm launches; -1 = default
- * (PGMI_VISION_LNFOLD env).
+ * 2 = LayerNorm2 only, with no in-launch hand-off: an unsplit out_proj stores per-row segment statistics
+ * that fc1's prologue combines; 0 (default: measured faster than both) = the separate split-K reduction +
+ * LayerNorm launches; -1 = default (PGMI_VISION_LNFOLD env).
  * Drops captured prefill graphs.  A tuning / test switch, no reference counterpart. */
 int pgmi_set_vision_lnfold(pgmi_ctx* ctx, int on);
 /* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden

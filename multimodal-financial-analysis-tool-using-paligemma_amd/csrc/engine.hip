@@ -687,7 +687,7 @@ static int run_graphed(pgmi_ctx* x, hipStream_t s, const std::vector<intptr_t>& 
 }  // extern "C++"
 
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats);
-static bool vision_lnfold(pgmi_ctx* x, int rows);
+static int vision_lnfold(pgmi_ctx* x, int rows);
 static int ensure_vision_fold(pgmi_ctx* x);
 
 int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, void* stream) {
@@ -709,6 +709,8 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
 // their split-K partials in the GEMM's last-arriving workgroup per tile and leave each row's LayerNorm
 // (mean, rstd); q|k|v and fc1 read the raw residual rows and apply the LayerNorm in their epilogue
 // through folded weights (kernels_gemm.hip gemm_res_ln / gemm_lnfold): two launches fewer per layer.
+// Mode 2 (LayerNorm2 only, hand-off free: unsplit out_proj segment statistics, fc1 prologue) measured
+// slower too: tower 1.50-1.52 -> 1.59-1.62 ms (profiles/r04_vision_ln2_stats_ab.txt).
 // Measured slower, off by default (PGMI_VISION_LNFOLD=1 or pgmi_set_vision_lnfold(ctx, 1) turns it on;
 // profiles/r04_vision_lnfold_ab.txt): the two in-launch hand-offs per residual projection (write-through
 // partials -> tile arrival -> coherent reads; segment statistics -> row-tile arrival) cost more than the
@@ -756,17 +758,37 @@ static void res_ln_args(pgmi_ctx* x, EpiArgs& e, float eps) {
     e.ln_eps = eps;
 }
 
-static bool vision_lnfold(pgmi_ctx* x, int rows) {
-    static const bool env = [] { const char* e = getenv("PGMI_VISION_LNFOLD"); return e && atoi(e) != 0; }();
-    const bool on = x->vision_lnfold < 0 ? env : x->vision_lnfold != 0;
+// gemm_lnfold's segment-record form needs fc1's plan to be P96x64s4 (BM <= 128 prologue): a dry call with
+// segment records set answers it
+static bool choose_is_p96(int rows, int N, int K) {
+    EpiArgs e{};
+    float dummy = 0.f;
+    e.lnst = &dummy;
+    e.lnseg = K / 32;
+    return gemm_lnfold(nullptr, nullptr, K, nullptr, rows, N, K, true, e, true);
+}
+
+static int vision_lnfold_mode(pgmi_ctx* x) {
+    static const int env = [] { const char* e = getenv("PGMI_VISION_LNFOLD"); return e ? atoi(e) : 0; }();
+    return x->vision_lnfold < 0 ? env : x->vision_lnfold;
+}
+
+// 0: off; 1: both LayerNorms folded (gemm_res_ln hand-offs); 2: LayerNorm2 only, hand-off free -- an unsplit
+// out_proj stores segment statistics (gemm_res_stats) that fc1's prologue combines (gemm_lnfold, lnseg)
+static int vision_lnfold(pgmi_ctx* x, int rows) {
+    const int mode = vision_lnfold_mode(x);
     const pgmi_config& c = x->c;
-    if (!on || rows != n_img(c) || c.v_layers < 2) return false;
+    if (mode <= 0 || mode > 2 || rows != n_img(c) || c.v_layers < 2) return 0;
     const int D = c.v_hidden, Iv = c.v_intermediate;
     EpiArgs e{};
+    if (!gemm_lnfold(nullptr, nullptr, D, nullptr, rows, Iv, D, true, e, true)) return 0;
+    if (mode == 2)
+        return D % 32 == 0 && choose_is_p96(rows, Iv, D) && gemm_res_stats(nullptr, nullptr, D, nullptr, rows, D, D, e, true)
+                   ? 2 : 0;
     return gemm_lnfold(nullptr, nullptr, D, nullptr, rows, 3 * D, D, false, e, true) &&
-           gemm_lnfold(nullptr, nullptr, D, nullptr, rows, Iv, D, true, e, true) &&
-           gemm_res_ln(nullptr, nullptr, D, nullptr, rows, D, D, e, x->ws, x->ws_bytes, true) > 0 &&
-           gemm_res_ln(nullptr, nullptr, Iv, nullptr, rows, D, Iv, e, x->ws, x->ws_bytes, true) > 0;
+                   gemm_res_ln(nullptr, nullptr, D, nullptr, rows, D, D, e, x->ws, x->ws_bytes, true) > 0 &&
+                   gemm_res_ln(nullptr, nullptr, Iv, nullptr, rows, D, Iv, e, x->ws, x->ws_bytes, true) > 0
+               ? 1 : 0;
 }
 
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats) {
@@ -787,7 +809,8 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
     // split-K reduction + bias + residual (splitk_res_norm), or, under vision_lnfold, computed as row
     // statistics by that projection (gemm_res_ln) and applied by the next one (gemm_lnfold)
     layernorm(s, x->vX, VL(x, 0, "layer_norm1.weight"), VL(x, 0, "layer_norm1.bias"), eps, x->vT, rows, D);
-    const bool fold = x->vfold_ready && vision_lnfold(x, rows);
+    const int fmode = x->vfold_ready ? vision_lnfold(x, rows) : 0;
+    const bool fold = fmode == 1, fold2 = fmode == 2;
     for (int i = 0; i < c.v_layers; ++i) {
         const bool last = i + 1 == c.v_layers;
         EpiArgs q{};
@@ -816,6 +839,9 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
         if (fold) {
             res_ln_args(x, o, eps);
             gemm_res_ln(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), rows, D, D, o, x->ws, x->ws_bytes);
+        } else if (fold2) {
+            o.lnst = x->vLnSt;
+            gemm_res_stats(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), rows, D, D, o);
         } else {
             int sp = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
                           x->ws_bytes, 0, true);
@@ -824,8 +850,14 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
         }
         EpiArgs f1{};
         f1.bias = VL(x, i, "mlp.fc1.bias"); f1.out = x->vH; f1.ldo = Iv;
-        if (fold) {
-            f1.lnmr = x->vLnMr;
+        if (fold || fold2) {
+            if (fold) {
+                f1.lnmr = x->vLnMr;
+            } else {
+                f1.lnst = x->vLnSt;
+                f1.lnseg = D / 32;
+                f1.ln_eps = eps;
+            }
             f1.lnc1 = x->vCfc1 + (long)i * 2 * Iv;
             f1.lnc0 = f1.lnc1 + Iv;
             gemm_lnfold(s, x->vX, D, x->vWfc1_f + (long)i * Iv * D, rows, Iv, D, true, f1);
@@ -1135,7 +1167,7 @@ int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
 
 int pgmi_set_vision_lnfold(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
-    x->vision_lnfold = on < 0 ? -1 : on != 0;
+    x->vision_lnfold = on < 0 ? -1 : on;
     clear_pgraphs(x);  // captured towers hold the other form's launches
     return 0;
 }

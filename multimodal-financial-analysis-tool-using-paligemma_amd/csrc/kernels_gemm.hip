@@ -96,16 +96,18 @@ __device__ __forceinline__ void epi_load(const EpiArgs& ea, int M, int N, int mb
         }
     }
     if constexpr (E::HL) {
+        if (!ea.lnst) {  // (segment records: k_gemm_p's prologue fills mu / rs from LDS)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int m = mb + i * 16 + (lane >> 4) * 4 + r;
-                m = m < M ? m : M - 1;
-                const float2 v = *reinterpret_cast<const float2*>(ea.lnmr + 2 * (long)m);
-                e.mu[i][r] = v.x;
-                e.rs[i][r] = v.y;
-            }
+                for (int r = 0; r < 4; ++r) {
+                    int m = mb + i * 16 + (lane >> 4) * 4 + r;
+                    m = m < M ? m : M - 1;
+                    const float2 v = *reinterpret_cast<const float2*>(ea.lnmr + 2 * (long)m);
+                    e.mu[i][r] = v.x;
+                    e.rs[i][r] = v.y;
+                }
+        }
     }
     if constexpr (E::HX) {
 #pragma unroll
@@ -609,6 +611,70 @@ __device__ __forceinline__ void res_ln_tail(const EpiArgs& ea, const float* __re
     ea.lnmr[2 * (long)m + 1] = 1.0f / sqrtf(m2 / (float)N + ea.ln_eps);
 }
 
+// gemm_res_stats epilogue: per row and 32-column segment of the bf16 result (the wave's TN x 16
+// columns of 4 rows per lane group), (sum, sum of squared deviations from the segment mean), plain stores
+template <int TM, int TN>
+__device__ __forceinline__ void seg_stats(const EpiArgs& ea, int M, int N, int mb, int seg, int lane,
+                                          const EpiOps<EPI_BIAS_RES, TM, TN>& e, const f32x4 (&acc)[TM][TN]) {
+    constexpr int SEGW = TN * 16;
+    const int nseg = N / SEGW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float x[TN], sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                x[j] = bf2f(f2bf(rbf(acc[i][j][r] + e.bv[j]) + e.xv[i][j][r]));  // the stored value
+                sm += x[j];
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+            const float mean = sm / (float)SEGW;
+            float d2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const float d = x[j] - mean;
+                d2 += d * d;
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
+            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            if ((lane & 15) == 0 && m < M)
+                *reinterpret_cast<float2*>(ea.lnst + ((long)m * nseg + seg) * 2) = make_float2(sm, d2);
+        }
+}
+
+// gemm_lnfold's prologue over segment records: thread t < BM combines row m0 + t's lnseg records (fixed
+// order, Chan's pairwise form) into (mean, rstd) in LDS
+template <int BM>
+__device__ __forceinline__ void ln_rows_prologue(const EpiArgs& ea, int M, int D, int m0, float* lds_mr) {
+    const int t = threadIdx.x;
+    if (t < BM) {
+        int m = m0 + t;
+        m = m < M ? m : M - 1;
+        const int nseg = ea.lnseg;
+        float2 v[kResLnSegs];
+#pragma unroll
+        for (int g = 0; g < kResLnSegs; ++g)
+            v[g] = *reinterpret_cast<const float2*>(ea.lnst + ((long)m * nseg + (g < nseg ? g : nseg - 1)) * 2);
+        float tot = 0.f;
+#pragma unroll
+        for (int g = 0; g < kResLnSegs; ++g) tot = g < nseg ? tot + v[g].x : tot;
+        const float mean = tot / (float)D;
+        const float segw = (float)(D / nseg);
+        float m2 = 0.f;
+#pragma unroll
+        for (int g = 0; g < kResLnSegs; ++g) {
+            const float dm = v[g].x / segw - mean;
+            m2 = g < nseg ? m2 + (v[g].y + segw * dm * dm) : m2;
+        }
+        lds_mr[2 * t] = mean;
+        lds_mr[2 * t + 1] = 1.0f / sqrtf(m2 / (float)D + ea.ln_eps);
+    }
+    __syncthreads();
+}
+
 template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
@@ -722,6 +788,20 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     // epilogue operands first (see epi_load): held in registers through the k loop
     const int epi_mb = m0 + wm * TM * 16, epi_nb = n0 + wn * TN * 16;
     EpiOps<EPI, TM, TN> epi_ops;
+    if constexpr (!SPLIT && (EPI == EPI_LNB || EPI == EPI_LNB_GELU)) {
+        __shared__ float ln_mr[2 * BM];
+        if (ea.lnst) {
+            ln_rows_prologue<BM>(ea, M, K, m0, ln_mr);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int lr = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+                    epi_ops.mu[i][r] = ln_mr[2 * lr];
+                    epi_ops.rs[i][r] = ln_mr[2 * lr + 1];
+                }
+        }
+    }
     if constexpr (!SPLIT) epi_load<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops);
     RopeOps<EPI == EPI_ROPE ? TM : 1> rope_ops;
     if constexpr (!SPLIT && EPI == EPI_ROPE) rope_load<TM, BN>(ea, M, epi_mb, epi_nb, lane, rope_ops);
@@ -792,6 +872,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
         rope_apply<TM>(ea, M, epi_mb, lane, rope_ops, acc[0]);
     } else {
         epi_apply<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops, acc[0], acc[NB - 1]);
+        if constexpr (EPI == EPI_BIAS_RES && NB == 1)
+            if (ea.lnst) seg_stats<TM, TN>(ea, M, N, epi_mb, nt * WN + wn, lane, epi_ops, acc[0]);
     }
 }
 
@@ -1800,10 +1882,20 @@ int gemm_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, in
     }
 }
 
+bool gemm_res_stats(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
+                    const EpiArgs& ea, bool dry) {
+    // P32x64s4 unsplit (the fastest unsplit out_proj of the round-3 sweep): 32-column segments
+    if (N % 64 != 0 || N / 32 > kResLnSegs) return false;
+    if (dry) return true;
+    launch_p<4, 2, 1, 2, 4, EPI_BIAS_RES>(s, A, lda, W, K, M, N, K, ea, nullptr, 1, 0);
+    return true;
+}
+
 bool gemm_lnfold(hipStream_t s, const uint16_t* A, int lda, const uint16_t* Wf, int M, int N, int K, bool gelu,
                  const EpiArgs& ea, bool dry) {
     const Plan p = choose(M, N, K, false);
     if (p.split != 1) return false;
+    if (ea.lnst && (K % 32 != 0 || K / 32 != ea.lnseg || p.cfg != P96x64s4)) return false;  // BM <= 128 prologue
 #define F_(wm, tm, tn, st)                                                                                       \
     do {                                                                                                         \
         if (dry) break;                                                                                          \

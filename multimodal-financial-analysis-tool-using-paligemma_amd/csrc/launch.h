@@ -54,6 +54,9 @@ struct EpiArgs {
     float ln_eps = 0.f;
     const float* lnc1 = nullptr;    // [N] sum_k W'[n][k]     (W' = bf16(W diag(gamma)))
     const float* lnc0 = nullptr;    // [N] sum_k beta_k W[n][k] + bias[n]
+    // gemm_res_stats / gemm_lnfold with lnseg > 0: the rows' statistics as lnseg 32-column segment
+    // records in lnst (written by the producer's epilogue), combined by the consumer's prologue
+    int lnseg = 0;
 };
 
 // C[M,N] = A[M,K] (row-major, lda) x W[N,K]^T (row-major, ldw).  For EPI_GEGLU the
@@ -76,6 +79,11 @@ size_t gemm_ws_bytes(int M, int N, int K);
 constexpr int kResLnTiles = 1024, kResLnRowTiles = 64, kResLnSegs = 48;  // counter / statistics capacity
 int gemm_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
                 const EpiArgs& ea, float* ws, size_t ws_bytes, bool dry = false);
+// unsplit residual projection (EPI_BIAS_RES) whose epilogue also stores each row's 32-column segment
+// (sum, sum of squared deviations) of the bf16 result to ea.lnst (plain stores, no hand-off inside the
+// launch); false = no such form for the shape (nothing launched)
+bool gemm_res_stats(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
+                    const EpiArgs& ea, bool dry = false);
 // LN(x) W^T + bias as r_m (x W'^T - mu_m c1) + c0 over the raw rows x (EPI_LNB / EPI_LNB_GELU);
 // false = no fold form for the shape's plan (nothing launched)
 bool gemm_lnfold(hipStream_t s, const uint16_t* A, int lda, const uint16_t* Wf, int M, int N, int K, bool gelu,

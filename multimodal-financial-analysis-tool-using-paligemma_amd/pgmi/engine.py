@@ -341,7 +341,8 @@ class Engine:
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
 
     def set_vision_lnfold(self, on: int) -> None:
-        """SigLIP LayerNorm fold (one image): 1 on, 0 separate LayerNorm launches (default), -1 default."""
+        """SigLIP LayerNorm fold (one image): 1 both LayerNorms, 2 LayerNorm2 via out_proj segment statistics,
+        0 separate LayerNorm launches (default), -1 default."""
         N.check(self.lib.pgmi_set_vision_lnfold(self.ctx, int(on)), "pgmi_set_vision_lnfold")
 
     def set_decode_staged_norm(self, on: int) -> None:

@@ -85,19 +85,21 @@ def test_teacher_forced_64_steps(eng224, G):
     _teacher_forced(eng224, G, G["bf16"], G["fp32"], 64)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @torch.no_grad()
-def test_vision_lnfold_vs_separate_layernorm(eng224, G):
-    """The one-image SigLIP tower with its LayerNorms folded into q|k|v / fc1 (opt-in, measured slower:
-    weights bf16(W diag(gamma)), statistics from the residual projections' last-arriving workgroups)
-    against the default separate split-K reduction + LayerNorm launches: the same features up to bf16
-    rounding, deterministic, and the folded tower's logits pass the 224 parity rules."""
+def test_vision_lnfold_vs_separate_layernorm(eng224, G, mode):
+    """The one-image SigLIP tower with its LayerNorms folded into the next projection (weights
+    bf16(W diag(gamma))): mode 1 both, statistics from the residual projections' last-arriving
+    workgroups; mode 2 LayerNorm2 only, statistics stored by an unsplit out_proj's epilogue and combined
+    by fc1's prologue.  Against the separate split-K reduction + LayerNorm launches: the same features
+    up to bf16 rounding, deterministic, and the tower's logits pass the 224 parity rules."""
     px = _px(G, "u8_0_224")
     b = eng224.vision(px).float().clone()
-    eng224.set_vision_lnfold(1)
+    eng224.set_vision_lnfold(mode)
     try:
         a = eng224.vision(px).float().clone()
         c = eng224.vision(px).float().clone()
-        _teacher_forced(eng224, G, G["bf16"], G["fp32"], 16, label="full224/lnfold")
+        _teacher_forced(eng224, G, G["bf16"], G["fp32"], 16, label=f"full224/lnfold{mode}")
     finally:
         eng224.set_vision_lnfold(-1)
     assert torch.equal(a, c)  # deterministic (fixed-order reductions, no float atomics)

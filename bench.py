@@ -20,7 +20,8 @@ images per GPU, and value = tokens of all ranks / the max-over-ranks timed regio
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline      the dominant decode kernel (fused RMSNorm + gate/up GEMV + GeGLU), timed with
                 HIP events on its own stream, algorithmic bytes per launch / average duration
-  cpu_baseline  the numpy oracle (oracle/paligemma_np.py) decoding on this host's cores
+  cpu_baseline  the decode step on this host's cores: a torch bf16 port (oracle/torch_cpu.py), with the
+                numpy oracle (oracle/paligemma_np.py) and the survey container's reference figure beside it
 """
 from __future__ import annotations
 
@@ -70,15 +71,38 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, seed, L, steps):
-    """The oracle (numpy restatement of modeling_gemma.py) decoding at the full 3B text shapes
-    on the host: bounded sample of `steps` KV-cached decode tokens after a synthetic cache of
-    L tokens (the decode path is what the metric counts; the prefill is not re-run)."""
+def cpu_baseline(cfg, seed, L, steps, torch_steps=32):
+    """The decode step on this host's cores, beside the GPU number (never the GPU's work):
+      value  oracle/torch_cpu.py -- a builder-written torch bf16 restatement of the KV-cached decode step
+             (full PaliGemma-3B text shapes, batch 1, cache of L tokens), `torch_steps` greedy steps;
+      numpy_port  the numpy oracle (oracle/paligemma_np.py: fp32 math with the reference's bf16 rounding
+             points) over a bounded `steps` sample;
+      reference_cpu  the reference's own modules as timed in the survey container (they cannot travel)."""
     import numpy as np
     import threadpoolctl
+    import torch
 
     from oracle import paligemma_np as O
     from oracle import weights as OW
+    from oracle.torch_cpu import TorchCpuDecoder
+    # torch port: the box's CPU share (16 threads; nproc shows the whole machine)
+    threads = min(16, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    t0 = time.time()
+    dec = TorchCpuDecoder(cfg, seed, max_kv=L + torch_steps + 8)
+    tgen_s = time.time() - t0
+    dec.fill_cache(L)
+    tok = 108
+    for s_ in range(2):  # warm (page in weights, oneDNN primitives)
+        tok = int(dec.step(tok, L + 1 + s_).argmax())
+    t0 = time.perf_counter()
+    for s_ in range(torch_steps):
+        tok = int(dec.step(tok, L + 3 + s_).argmax())
+    torch_dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
+    del dec
+
     t0 = time.time()
     shapes = {n: s for n, s in OW.param_shapes(cfg).items() if n.startswith("language_model")}
     P = {n: OW.gen_f32(n, s, seed) for n, s in shapes.items()}
@@ -96,15 +120,19 @@ def cpu_baseline(cfg, seed, L, steps):
         lg = O.paligemma_decode(P, cfg, tok, kv, L + 2 + s)
         tok = np.argmax(lg[:, -1], -1)
     dt = time.perf_counter() - t0
-    threads = max([i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()] or [1])
-    return {"value": round(steps / dt, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+    np_threads = max([i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()] or [1])
+    return {"value": round(torch_steps / torch_dt, 3), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+            "sample": f"{torch_steps} KV-cached greedy decode steps of oracle/torch_cpu.py (torch {torch.__version__} "
+                      f"CPU, bf16 weights and activations, the reference's rounding points) at full PaliGemma-3B "
+                      f"text shapes, batch 1, cache {L} tokens, {threads} threads; weight generation ({tgen_s:.0f}s) "
+                      f"untimed",
+            "numpy_port": {"value": round(steps / dt, 4), "unit": "tokens/s", "cores": int(np_threads),
+                           "sample": f"{steps} decode steps of oracle/paligemma_np.py (numpy fp32 math, bf16 rounding "
+                                     f"points), same shapes and cache; weight generation ({gen_s:.0f}s) untimed"},
             "reference_cpu": {"value": 12.2, "unit": "tokens/s", "cores": 8, "dtype": "bf16",
                               "inference_py_semantics_tok_s": 5.2, "prefill_ms": 640,
                               "where": "the reference's own modules timed in the survey container (8 Xeon cores, "
-                                       "torch 2.10 CPU), BASELINE.md sec.2; the reference cannot travel to the GPU box"},
-            "sample": f"{steps} KV-cached greedy decode steps of oracle/paligemma_np.py (numpy fp32 with bf16 "
-                      f"rounding points) at full PaliGemma-3B text shapes, batch 1, cache {L} tokens; "
-                      f"weight generation ({gen_s:.0f}s) untimed"}
+                                       "torch 2.10 CPU), BASELINE.md sec.2; the reference cannot travel to the GPU box"}}
 
 
 MFMA_BF16_PEAK_TFS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
@@ -413,23 +441,39 @@ def time_api(cfg, dev, seed, tokens):
                 ts.append((time.perf_counter() - t0) * 1e3)
             res[f"prefill_ms_{mode}_logits"] = round(statistics.median(ts), 3)
         m.pgmi_prefill_logits = "lazy"
-        ids, mask = ids0, torch.ones_like(ids0)
-        out, kv = prefill("lazy")
-        n = 0
-        t0 = None
-        for step in range(tokens + 4):
-            if step == 4:
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-            nxt = torch.argmax(out["logits"][:, -1, :], dim=-1, keepdim=True).squeeze(0)
-            _ = nxt.item()
-            ids = nxt.unsqueeze(-1)
-            mask = torch.cat([mask, torch.ones((1, 1), device=dev)], dim=-1)
-            out = m(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
-            n += step >= 4
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+
+        def decode_run():
+            ids, mask = ids0, torch.ones_like(ids0)
+            out, kv = prefill("lazy")
+            n = 0
+            t0 = None
+            for step in range(tokens + 4):
+                if step == 4:
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                nxt = torch.argmax(out["logits"][:, -1, :], dim=-1, keepdim=True).squeeze(0)
+                _ = nxt.item()
+                ids = nxt.unsqueeze(-1)
+                mask = torch.cat([mask, torch.ones((1, 1), device=dev)], dim=-1)
+                out = m(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
+                n += step >= 4
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0, n
+
+        # the binding's submission form (pgmi/binding.py DROPIN_DECODE_SPLIT) and the alternatives beside it:
+        # one graph per step vs two (the step's head + k layers first), alternating, best of 3 each
+        default_split = eng.decode_split
+        split_ms = {}
+        for rep in range(3):
+            for k in (0, 1, 2, 4):
+                eng.set_decode_split(k)
+                dt, n = decode_run()
+                split_ms.setdefault(k, []).append(dt * 1e3 / n)
+        eng.set_decode_split(default_split)
+        dt, n = decode_run()
     res.update(decode_ms_per_token=round(dt * 1e3 / n, 4), decode_tok_s=round(n / dt, 1), tokens_timed=n,
+               decode_split=default_split,
+               decode_split_ms_per_token={str(k): round(min(v), 4) for k, v in split_ms.items()},
                semantics="inference.py:55-78 through the drop-in module: pixel_values re-passed, float mask column "
                          "appended, argmax of logits[:, -1, :], .item() per token")
     res["ablation_harness"] = time_ablation(m, ids0, px, tokens)

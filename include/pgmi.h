@@ -159,17 +159,16 @@ int pgmi_decode_embeds_dev(pgmi_ctx* ctx, const void* embeds, int B, void* kv, i
 int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
 /* Batched decode (B >= 3, MFMA projections) RMSNorm form: 0 = each input norm computed once per row
  * and read unstaged by the q|k|v / gate|up projections (default), 1 = staged inside each projection,
- * -1 = back to the default (PGMI_MF_STAGED env).  Same arithmetic either way (bf16 normalised rows);
+ * -1 = back to the default.  Same arithmetic either way (bf16 normalised rows);
  * drops captured decode graphs.  A tuning / test switch, no reference counterpart. */
 int pgmi_set_decode_staged_norm(pgmi_ctx* ctx, int on);
-/* SigLIP LayerNorm fold at the one-image plan: 1 = out_proj / fc2 reduce their split-K
- * partials in the GEMM with the next LayerNorm's row statistics, and q|k|v / fc1 apply that LayerNorm
- * in their epilogue through weights folded at pgmi_prepare (bf16(W diag(gamma)), fp32 column terms);
- * 2 = LayerNorm2 only, with no in-launch hand-off: an unsplit out_proj stores per-row segment statistics
- * that fc1's prologue combines; 0 (default: measured faster than both) = the separate split-K reduction +
- * LayerNorm launches; -1 = default (PGMI_VISION_LNFOLD env).
- * Drops captured prefill graphs.  A tuning / test switch, no reference counterpart. */
-int pgmi_set_vision_lnfold(pgmi_ctx* ctx, int on);
+/* Submission form of the graphed decode step (pgmi_decode*, use_graph != 0): layers > 0 captures the step
+ * as two graphs -- the head (embedding, first norm) with the first `layers` layers, then the other layers
+ * with the final norm, lm_head and argmax -- launched back to back, so the GPU starts after a short first
+ * submission while the host still submits the second (a caller that waits on every token, inference.py:68's
+ * .item(), hides most of the submission); 0 = one graph (default).  The same kernels in the same order:
+ * outputs are bit-identical.  Drops captured decode graphs.  A tuning switch, no reference counterpart. */
+int pgmi_set_decode_split(pgmi_ctx* ctx, int layers);
 /* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden
  * rows: logits (device fp32 [rows][vocab]) = fp32(bf16(normed . E^T)) with the tied embedding E.
  * Together with pgmi_lm_final_hidden this materialises the prefill's all-row logits on demand
@@ -238,6 +237,12 @@ int pgmi_tune_gemm(int cfg, int split);
  * Split-K partials that a consumer reduces (out_proj, fc2, down: the residual + norm kernel) are
  * limited to 16 slabs. */
 int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split);
+
+/* Test hook: the workgroup -> (row tile, column tile, K slice) order of a panel / 8-phase prefill GEMM
+ * launch of n_mt x n_nt tiles x S K slices (tile BM x BN, K deep), as the kernels compute it (the XCD
+ * block raster of kernels_gemm.hip xcd_tile); mt/nt/z receive n_mt*n_nt*S entries indexed by the linear
+ * workgroup id.  Returns the XCD block code the launch uses (0 = run order); no device needed. */
+int pgmi_debug_gemm_tiles(int n_mt, int n_nt, int S, int BM, int BN, int K, int* mt, int* nt, int* z);
 
 /* Tuning hook: force the prefill attention kernel (kernels_attn.hip): 0 = 16-row kernel with
  * LDS-resident scores, 7 = one pass with K/V loaded once and scores in registers (head_dim 72, <= 256 keys),

@@ -72,6 +72,7 @@ struct GraphKey {
 struct GraphEntry {
     int seen = 0;
     hipGraphExec_t exec = nullptr;
+    hipGraphExec_t exec2 = nullptr;  // the split submission's second graph (decode_split)
 };
 
 struct pgmi_ctx {
@@ -97,14 +98,6 @@ struct pgmi_ctx {
     int64_t* dids_tmp;
     // vision workspace (rows = max_batch*N)
     uint16_t *vX, *vT, *vQKV, *vAO, *vH, *vP;
-    // SigLIP LayerNorms folded into q|k|v and fc1 (one-image plan, vision_lnfold): per layer the folded
-    // weights bf16(W diag(gamma)) and (c1, c0); the residual projections' row statistics and counters
-    uint16_t *vWqkv_f = nullptr, *vWfc1_f = nullptr;
-    float *vCqkv = nullptr, *vCfc1 = nullptr;  // [layer][2][N]: c1 then c0
-    float *vLnSt = nullptr, *vLnMr = nullptr;
-    unsigned *vTcnt = nullptr, *vRcnt = nullptr;
-    int vision_lnfold = -1;  // -1: PGMI_VISION_LNFOLD (default off: measured slower)
-    bool vfold_ready = false;
     float* ws;
     size_t ws_bytes;
     // decode workspace
@@ -128,7 +121,10 @@ struct pgmi_ctx {
     // identical pointer/shape arguments (a replay is the eager call: kernels read the same
     // addresses at run time), captured on the second such call
     bool prefill_graph = true;
-    int mf_staged = -1;  // batched decode RMSNorm form (mf_staged()); -1 = PGMI_MF_STAGED / default
+    int mf_staged = -1;  // batched decode RMSNorm form (mf_staged()); -1 = default (unstaged)
+    // graphed decode step submitted as two graphs (pgmi_set_decode_split): the first holds the step's head and
+    // this many layers, so the GPU starts while the host still submits the rest; 0 = one graph
+    int decode_split = 0;
     // device step state as the last enqueued per-phase decode step leaves it (advanced in-graph)
     bool step_known = false;
     int step_kv = 0, step_pos = 0;
@@ -137,6 +133,7 @@ struct pgmi_ctx {
     // GEMM (ev[4i], ev[4i+1]) and down GEMM (ev[4i+2], ev[4i+3]) of eager forwards
     std::vector<hipEvent_t> probe_ev;
     bool probe_on = false;
+    bool graph_before_probe = true;  // prefill_graph as the caller left it before the probe turned it off
 };
 
 namespace {
@@ -145,6 +142,15 @@ void clear_pgraphs(pgmi_ctx* x) {
     for (auto& kv : x->pgraphs)
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
     x->pgraphs.clear();
+}
+
+// the captured decode steps (one or two graphs each)
+void clear_dgraphs(pgmi_ctx* x) {
+    for (auto& kv : x->graphs) {
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        if (kv.second.exec2) (void)hipGraphExecDestroy(kv.second.exec2);
+    }
+    x->graphs.clear();
 }
 
 int n_img(const pgmi_config& c) { return (c.v_image / c.v_patch) * (c.v_image / c.v_patch); }
@@ -362,8 +368,7 @@ int pgmi_destroy(pgmi_ctx* x) {
     if (x)
         for (auto& e : x->probe_ev) (void)hipEventDestroy(e);
     if (!x) return 0;
-    for (auto& kv : x->graphs)
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    clear_dgraphs(x);
     clear_pgraphs(x);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->cap_stream) (void)hipStreamDestroy(x->cap_stream);
@@ -388,9 +393,7 @@ int pgmi_bind_weights(pgmi_ctx* x, void* slab) {
     if (!x || !slab) return fail(PGMI_E_ARG, "null argument");
     if (reinterpret_cast<uintptr_t>(slab) % 256 != 0) return fail(PGMI_E_ARG, "weight slab must be 256-byte aligned");
     x->slab = reinterpret_cast<uint8_t*>(slab);
-    for (auto& kv : x->graphs)
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-    x->graphs.clear();
+    clear_dgraphs(x);
     clear_pgraphs(x);
     return 0;
 }
@@ -628,7 +631,6 @@ int pgmi_prepare(pgmi_ctx* x) {
     // derived tensors
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
-    x->vfold_ready = false;  // vision_lnfold's folded projections: rebuilt from these weights on first use
     LAUNCHCHK();
     std::vector<uint16_t> cs, sn;
     if (!x->host_cos.empty()) {
@@ -640,9 +642,7 @@ int pgmi_prepare(pgmi_ctx* x) {
     HIPCHK(hipMemcpy(x->cosT, cs.data(), cs.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(x->sinT, sn.data(), sn.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipDeviceSynchronize());
-    for (auto& kv : x->graphs)
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-    x->graphs.clear();
+    clear_dgraphs(x);
     clear_pgraphs(x);
     x->prepared = true;
     return 0;
@@ -687,8 +687,6 @@ static int run_graphed(pgmi_ctx* x, hipStream_t s, const std::vector<intptr_t>& 
 }  // extern "C++"
 
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats);
-static int vision_lnfold(pgmi_ctx* x, int rows);
-static int ensure_vision_fold(pgmi_ctx* x);
 
 int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, void* stream) {
     int rc;
@@ -696,99 +694,12 @@ int pgmi_vision(pgmi_ctx* x, const void* pixels, int dtype, int B, void* feats, 
     const pgmi_config& c = x->c;
     if (B < 1 || B > c.max_batch) return fail(PGMI_E_ARG, "batch exceeds max_batch");
     if (!pixels || !feats) return fail(PGMI_E_ARG, "null argument");
-    if (vision_lnfold(x, B * n_img(c)) && (rc = ensure_vision_fold(x))) return rc;
     const std::vector<intptr_t> key{1, (intptr_t)pixels, dtype, B, (intptr_t)feats};
     rc = run_graphed(x, (hipStream_t)stream, key,
                      [&](hipStream_t st) { return vision_body(x, st, pixels, dtype, B, feats); });
     if (rc) return rc;
     LAUNCHCHK();
     return 0;
-}
-
-// SigLIP LayerNorm fold (round 4): at the one-image plan the residual projections (out_proj, fc2) reduce
-// their split-K partials in the GEMM's last-arriving workgroup per tile and leave each row's LayerNorm
-// (mean, rstd); q|k|v and fc1 read the raw residual rows and apply the LayerNorm in their epilogue
-// through folded weights (kernels_gemm.hip gemm_res_ln / gemm_lnfold): two launches fewer per layer.
-// Mode 2 (LayerNorm2 only, hand-off free: unsplit out_proj segment statistics, fc1 prologue) measured
-// slower too: tower 1.50-1.52 -> 1.59-1.62 ms (profiles/r04_vision_ln2_stats_ab.txt).
-// Measured slower, off by default (PGMI_VISION_LNFOLD=1 or pgmi_set_vision_lnfold(ctx, 1) turns it on;
-// profiles/r04_vision_lnfold_ab.txt): the two in-launch hand-offs per residual projection (write-through
-// partials -> tile arrival -> coherent reads; segment statistics -> row-tile arrival) cost more than the
-// launch boundary they replace: out_proj 5.8 + 5.1 (reduction + LayerNorm) -> 16.8-18.5 us, fc2 12.3-13.6
-// + 5.8 -> 26.5-29.1 us, tower 1.51 -> 1.95-1.99 ms.  Shapes whose plans have no such form (448 px,
-// batched images) always keep splitk_res_norm.
-// the fold's buffers and folded weights, built on first use after each pgmi_prepare (outside any capture:
-// pgmi_vision calls it before run_graphed)
-static int ensure_vision_fold(pgmi_ctx* x) {
-    if (x->vfold_ready) return 0;
-    const pgmi_config& c = x->c;
-    const size_t D = c.v_hidden, Iv = c.v_intermediate, Lv = c.v_layers, N = n_img(c);
-    int rc;
-    if (!x->vWqkv_f) {
-        if ((rc = dalloc_t(x, &x->vWqkv_f, Lv * 3 * D * D))) return rc;
-        if ((rc = dalloc_t(x, &x->vWfc1_f, Lv * Iv * D))) return rc;
-        if ((rc = dalloc_t(x, &x->vCqkv, Lv * 2 * 3 * D))) return rc;
-        if ((rc = dalloc_t(x, &x->vCfc1, Lv * 2 * Iv))) return rc;
-        if ((rc = dalloc_t(x, &x->vLnSt, N * kResLnSegs * 2))) return rc;
-        if ((rc = dalloc_t(x, &x->vLnMr, N * 2))) return rc;
-        if ((rc = dalloc_t(x, &x->vTcnt, (size_t)kResLnTiles))) return rc;
-        if ((rc = dalloc_t(x, &x->vRcnt, (size_t)kResLnRowTiles))) return rc;
-        HIPCHK(hipMemset(x->vTcnt, 0, kResLnTiles * sizeof(unsigned)));
-        HIPCHK(hipMemset(x->vRcnt, 0, kResLnRowTiles * sizeof(unsigned)));
-    }
-    for (int i = 0; i < c.v_layers; ++i) {
-        ln_fold_weights(nullptr, VL(x, i, "self_attn.q_proj.weight"), VL(x, i, "layer_norm1.weight"),
-                        VL(x, i, "layer_norm1.bias"), VL(x, i, "self_attn.q_proj.bias"), (int)(3 * D), (int)D,
-                        x->vWqkv_f + i * 3 * D * D, x->vCqkv + i * 6 * D, x->vCqkv + i * 6 * D + 3 * D);
-        ln_fold_weights(nullptr, VL(x, i, "mlp.fc1.weight"), VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
-                        VL(x, i, "mlp.fc1.bias"), (int)Iv, (int)D, x->vWfc1_f + i * Iv * D, x->vCfc1 + i * 2 * Iv,
-                        x->vCfc1 + i * 2 * Iv + Iv);
-    }
-    LAUNCHCHK();
-    HIPCHK(hipDeviceSynchronize());
-    x->vfold_ready = true;
-    return 0;
-}
-
-static void res_ln_args(pgmi_ctx* x, EpiArgs& e, float eps) {
-    e.tcnt = x->vTcnt;
-    e.rcnt = x->vRcnt;
-    e.lnst = x->vLnSt;
-    e.lnmr = x->vLnMr;
-    e.ln_eps = eps;
-}
-
-// gemm_lnfold's segment-record form needs fc1's plan to be P96x64s4 (BM <= 128 prologue): a dry call with
-// segment records set answers it
-static bool choose_is_p96(int rows, int N, int K) {
-    EpiArgs e{};
-    float dummy = 0.f;
-    e.lnst = &dummy;
-    e.lnseg = K / 32;
-    return gemm_lnfold(nullptr, nullptr, K, nullptr, rows, N, K, true, e, true);
-}
-
-static int vision_lnfold_mode(pgmi_ctx* x) {
-    static const int env = [] { const char* e = getenv("PGMI_VISION_LNFOLD"); return e ? atoi(e) : 0; }();
-    return x->vision_lnfold < 0 ? env : x->vision_lnfold;
-}
-
-// 0: off; 1: both LayerNorms folded (gemm_res_ln hand-offs); 2: LayerNorm2 only, hand-off free -- an unsplit
-// out_proj stores segment statistics (gemm_res_stats) that fc1's prologue combines (gemm_lnfold, lnseg)
-static int vision_lnfold(pgmi_ctx* x, int rows) {
-    const int mode = vision_lnfold_mode(x);
-    const pgmi_config& c = x->c;
-    if (mode <= 0 || mode > 2 || rows != n_img(c) || c.v_layers < 2) return 0;
-    const int D = c.v_hidden, Iv = c.v_intermediate;
-    EpiArgs e{};
-    if (!gemm_lnfold(nullptr, nullptr, D, nullptr, rows, Iv, D, true, e, true)) return 0;
-    if (mode == 2)
-        return D % 32 == 0 && choose_is_p96(rows, Iv, D) && gemm_res_stats(nullptr, nullptr, D, nullptr, rows, D, D, e, true)
-                   ? 2 : 0;
-    return gemm_lnfold(nullptr, nullptr, D, nullptr, rows, 3 * D, D, false, e, true) &&
-                   gemm_res_ln(nullptr, nullptr, D, nullptr, rows, D, D, e, x->ws, x->ws_bytes, true) > 0 &&
-                   gemm_res_ln(nullptr, nullptr, Iv, nullptr, rows, D, Iv, e, x->ws, x->ws_bytes, true) > 0
-               ? 1 : 0;
 }
 
 static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype, int B, void* feats) {
@@ -806,25 +717,15 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
     gemm(s, x->vP, x->kpad, x->patch_w, x->kpad, rows, D, x->kpad, EPI_BIAS_POS, e, x->ws, x->ws_bytes);
     const float scale = (float)std::pow((double)(D / c.v_heads), -0.5);  // head_dim**-0.5 (:89)
     // LayerNorm1 of layer 0; every later LayerNorm is fused with the preceding projection's
-    // split-K reduction + bias + residual (splitk_res_norm), or, under vision_lnfold, computed as row
-    // statistics by that projection (gemm_res_ln) and applied by the next one (gemm_lnfold)
+    // split-K reduction + bias + residual (splitk_res_norm)
     layernorm(s, x->vX, VL(x, 0, "layer_norm1.weight"), VL(x, 0, "layer_norm1.bias"), eps, x->vT, rows, D);
-    const int fmode = x->vfold_ready ? vision_lnfold(x, rows) : 0;
-    const bool fold = fmode == 1, fold2 = fmode == 2;
     for (int i = 0; i < c.v_layers; ++i) {
         const bool last = i + 1 == c.v_layers;
         EpiArgs q{};
         q.bias = VL(x, i, "self_attn.q_proj.bias");  // q|k|v biases adjacent
         q.out = x->vQKV;
         q.ldo = 3 * D;
-        if (fold && i > 0) {
-            q.lnmr = x->vLnMr;
-            q.lnc1 = x->vCqkv + (long)i * 6 * D;
-            q.lnc0 = q.lnc1 + 3 * D;
-            gemm_lnfold(s, x->vX, D, x->vWqkv_f + (long)i * 3 * D * D, rows, 3 * D, D, false, q);
-        } else {
-            gemm(s, x->vT, D, VL(x, i, "self_attn.q_proj.weight"), D, rows, 3 * D, D, EPI_BIAS, q, x->ws, x->ws_bytes);
-        }
+        gemm(s, x->vT, D, VL(x, i, "self_attn.q_proj.weight"), D, rows, 3 * D, D, EPI_BIAS, q, x->ws, x->ws_bytes);
         AttnArgs a{};
         a.q = x->vQKV; a.q_b_stride = (long)N * 3 * D; a.q_row_stride = 3 * D; a.q_head_stride = 72;
         a.k = x->vQKV + D; a.k_b_stride = a.q_b_stride; a.k_row_stride = 3 * D; a.k_head_stride = 72;
@@ -836,41 +737,15 @@ static int vision_body(pgmi_ctx* x, hipStream_t s, const void* pixels, int dtype
         EpiArgs o{};
         o.bias = VL(x, i, "self_attn.out_proj.bias");
         o.res = x->vX; o.ldr = D; o.out = x->vX; o.ldo = D;
-        if (fold) {
-            res_ln_args(x, o, eps);
-            gemm_res_ln(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), rows, D, D, o, x->ws, x->ws_bytes);
-        } else if (fold2) {
-            o.lnst = x->vLnSt;
-            gemm_res_stats(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), rows, D, D, o);
-        } else {
-            int sp = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
-                          x->ws_bytes, 0, true);
-            splitk_res_norm(s, x->ws, sp, o.bias, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
-                            eps, x->vT, rows, D);
-        }
+        const int spo = gemm(s, x->vAO, D, VL(x, i, "self_attn.out_proj.weight"), D, rows, D, D, EPI_BIAS_RES, o, x->ws,
+                             x->ws_bytes, 0, true);
+        splitk_res_norm(s, x->ws, spo, o.bias, x->vX, VL(x, i, "layer_norm2.weight"), VL(x, i, "layer_norm2.bias"),
+                        eps, x->vT, rows, D);
         EpiArgs f1{};
         f1.bias = VL(x, i, "mlp.fc1.bias"); f1.out = x->vH; f1.ldo = Iv;
-        if (fold || fold2) {
-            if (fold) {
-                f1.lnmr = x->vLnMr;
-            } else {
-                f1.lnst = x->vLnSt;
-                f1.lnseg = D / 32;
-                f1.ln_eps = eps;
-            }
-            f1.lnc1 = x->vCfc1 + (long)i * 2 * Iv;
-            f1.lnc0 = f1.lnc1 + Iv;
-            gemm_lnfold(s, x->vX, D, x->vWfc1_f + (long)i * Iv * D, rows, Iv, D, true, f1);
-        } else {
-            gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
-        }
+        gemm(s, x->vT, D, VL(x, i, "mlp.fc1.weight"), D, rows, Iv, D, EPI_BIAS_GELU, f1, x->ws, x->ws_bytes);
         EpiArgs f2{};
         f2.bias = VL(x, i, "mlp.fc2.bias"); f2.res = x->vX; f2.ldr = D; f2.out = x->vX; f2.ldo = D;
-        if (fold && !last) {
-            res_ln_args(x, f2, eps);
-            gemm_res_ln(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), rows, D, Iv, f2, x->ws, x->ws_bytes);
-            continue;
-        }
         const int sp = gemm(s, x->vH, Iv, VL(x, i, "mlp.fc2.weight"), Iv, rows, D, Iv, EPI_BIAS_RES, f2, x->ws,
                             x->ws_bytes, 0, true);
         splitk_res_norm(s, x->ws, sp, f2.bias, x->vX,
@@ -1060,18 +935,20 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
 }
 
 // The batched form's RMSNorms: computed once per row (k_rows_norm / the down combine's fused norm) and read
-// unstaged by q|k|v and gate|up (default), or staged by each projection itself (PGMI_MF_STAGED=1).  Equal
+// unstaged by q|k|v and gate|up (default), or staged by each projection itself (pgmi_set_decode_staged_norm,
+// tested by test_batch_rows_teacher_forced_vs_own_reference[8-1]).  Equal
 // while the weight streams were non-temporal (B = 8 step 1.5449 vs 1.5452 ms); with the default cache policy
 // (kernels_gemv_mfma.hip PGMI_MF_NT) the unstaged form wins, same box: 1.4523 / 1.4550 -> 1.4330 / 1.4320 ms
-static bool mf_staged(const pgmi_ctx* x) {
-    static const bool env = [] { const char* e = getenv("PGMI_MF_STAGED"); return e && atoi(e) != 0; }();
-    return x->mf_staged < 0 ? env : x->mf_staged != 0;
-}
+static bool mf_staged(const pgmi_ctx* x) { return x->mf_staged > 0; }
 
+// part: 0 = the whole step; 1 = its head (embedding / first norm and layers [0, decode_split)); 2 = the rest
+// (layers [decode_split, L), final norm, lm_head, argmax) -- the two graphs of the split submission
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr,
-                       int masked = 0) {
+                       int masked = 0, int part = 0) {
     const pgmi_config& c = x->c;
+    const int lsplit = std::min(std::max(x->decode_split, 1), c.t_layers - 1);
+    const int l_begin = part == 2 ? lsplit : 0, l_end = part == 1 ? lsplit : c.t_layers;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const float eps = c.t_rms_eps;
     const float normalizer = bf16_round_host(std::sqrt((float)H));
@@ -1082,14 +959,16 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const bool fold = !embeds && gemv_qkv_folds_embed(B) && c.t_layers > 0;
     const EmbedFold emb{ids, E, normalizer, c.pad_token_id, x->dH};
     // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
-    if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
-    else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    if (part != 2) {
+        if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
+        else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
+    }
     // B >= 3 (MFMA projections): every RMSNorm is computed once per row (k_rows_norm after o_proj, fused
     // into the down projection's combine for the next layer's input norm) and the q|k|v and gate|up
     // projections read the normalised rows dHn without staging
     const bool mf = B >= gemv_mf_min_batch() && !mf_staged(x);
-    if (mf && c.t_layers > 0) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
-    for (int i = 0; i < c.t_layers; ++i) {
+    if (mf && c.t_layers > 0 && part != 2) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
+    for (int i = l_begin; i < l_end; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
         gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
@@ -1106,16 +985,9 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         } else {
             a.mask = x->d_zero; a.mask_b_stride = 0; a.mask_k_stride = 0; a.mask_round = 1;
         }
-        if (B >= gemv_mf_min_batch() && NKV == 1 && attn_comb_fused(B)) {
-            // the combine runs in the attention launch (its last chunk per row), o_proj reads dAO
-            attention_decode_comb(s, a, x->step, launch_keys, x->opart, x->max_chunks, x->arrive_rows);
-            gemv_o_attn(s, B, NH, nullptr, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                        x->dAO);
-        } else {
-            attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
-            gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                        B >= gemv_mf_min_batch() ? x->dAO : nullptr);
-        }
+        attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
+        gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
+                    B >= gemv_mf_min_batch() ? x->dAO : nullptr);
         if (mf) {
             rows_norm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, B, H, x->dHn);
             gemv_geglu(s, B, x->dHn, nullptr, eps, TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);
@@ -1127,6 +999,7 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
     }
+    if (part == 1) return 0;
     int nparts = 0;
     int64_t* nx = next_ids ? next_ids : x->d_next;
     // the step's last work also advances the device step state (pgmi_decode skips its host-side
@@ -1143,8 +1016,12 @@ int pgmi_prefill_probe(pgmi_ctx* x, int on) {
         x->probe_ev.resize((size_t)4 * x->c.t_layers);
         for (auto& e : x->probe_ev) HIPCHK(hipEventCreate(&e));
     }
+    // the probe records its events in eager forwards: prefill graphs are off while it is on, and the
+    // caller's own setting (pgmi_set_prefill_graph) is restored when it is turned off
+    if (on && !x->probe_on) x->graph_before_probe = x->prefill_graph;
+    if (!on && x->probe_on) x->prefill_graph = x->graph_before_probe;
     x->probe_on = on != 0;
-    x->prefill_graph = !x->probe_on;  // the probe records its events in eager forwards
+    if (x->probe_on) x->prefill_graph = false;
     clear_pgraphs(x);
     return 0;
 }
@@ -1165,25 +1042,25 @@ int pgmi_prefill_probe_times(pgmi_ctx* x, float* us, int n) {
     return 0;
 }
 
-int pgmi_set_vision_lnfold(pgmi_ctx* x, int on) {
-    if (!x) return fail(PGMI_E_ARG, "null context");
-    x->vision_lnfold = on < 0 ? -1 : on;
-    clear_pgraphs(x);  // captured towers hold the other form's launches
-    return 0;
-}
-
 int pgmi_set_decode_staged_norm(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
     x->mf_staged = on < 0 ? -1 : on != 0;
-    for (auto& kv : x->graphs)  // captured steps hold the other form's launches
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-    x->graphs.clear();
+    clear_dgraphs(x);  // captured steps hold the other form's launches
+    return 0;
+}
+
+int pgmi_set_decode_split(pgmi_ctx* x, int layers) {
+    if (!x) return fail(PGMI_E_ARG, "null context");
+    if (layers < 0) return fail(PGMI_E_ARG, "layers must be >= 0");
+    x->decode_split = layers;
+    clear_dgraphs(x);  // captured steps hold the other submission form
     return 0;
 }
 
 int pgmi_set_prefill_graph(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
-    x->prefill_graph = on != 0;
+    if (x->probe_on) x->graph_before_probe = on != 0;  // applied when the probe is turned off
+    else x->prefill_graph = on != 0;
     clear_pgraphs(x);
     return 0;
 }
@@ -1260,15 +1137,19 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
             return 0;
         }
         HIPCHK(hipStreamSynchronize(s));
-        hipGraph_t g;
-        HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked);
-        HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
-        if (rc) return rc;
-        HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
+        const bool two = x->decode_split > 0 && x->c.t_layers >= 2;
+        for (int p = two ? 1 : 0; p <= (two ? 2 : 0); ++p) {
+            hipGraph_t g;
+            HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
+            rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked, p);
+            HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
+            if (rc) return rc;
+            HIPCHK(hipGraphInstantiate(p == 2 ? &ge.exec2 : &ge.exec, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+        }
     }
     HIPCHK(hipGraphLaunch(ge.exec, s));
+    if (ge.exec2) HIPCHK(hipGraphLaunch(ge.exec2, s));
     LAUNCHCHK();
     advanced();
     return 0;
@@ -1483,6 +1364,11 @@ int pgmi_prefill_kernel(pgmi_ctx* x, int which, int layer, int rows, void* strea
     }
     LAUNCHCHK();
     return 0;
+}
+
+int pgmi_debug_gemm_tiles(int n_mt, int n_nt, int S, int BM, int BN, int K, int* mt, int* nt, int* z) {
+    if (n_mt < 1 || n_nt < 1 || S < 1 || !mt || !nt || !z) return fail(PGMI_E_ARG, "bad argument");
+    return gemm_tile_order(n_mt, n_nt, S, BM, BN, K, mt, nt, z);
 }
 
 int pgmi_tune_gemm(int cfg, int split) {

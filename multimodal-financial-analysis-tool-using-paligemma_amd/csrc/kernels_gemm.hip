@@ -12,12 +12,12 @@
 // on distinct banks.  Split-K (grid.z) writes fp32 partial slabs that a separate
 // epilogue kernel reduces in a fixed order (bitwise reproducible).
 #include <map>
+#include <mutex>
 #include <tuple>
 #include <vector>
 
 #include <hip/hip_ext.h>
 
-#include "coh.h"
 #include "common.h"
 #include "launch.h"
 
@@ -45,12 +45,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float
             break;
         case EPI_F32: ea.out_f32[(long)m * ea.ldo + n] = rbf(acc); break;
         case EPI_GEGLU: ea.out[(long)m * ea.ldo + n] = f2bf(rbf(gelu_tanh(rbf(acc))) * rbf(acc2)); break;
-        case EPI_LNB:
-        case EPI_LNB_GELU: {
-            const float o = ea.lnmr[2 * m + 1] * (acc - ea.lnmr[2 * m] * ea.lnc1[n]) + ea.lnc0[n];
-            ea.out[(long)m * ea.ldo + n] = f2bf(EPI == EPI_LNB ? o : gelu_tanh(rbf(o)));
-            break;
-        }
+        default: break;  // EPI_ROPE: rope_apply
     }
 }
 
@@ -73,11 +68,8 @@ template <int EPI, int TM, int TN>
 struct EpiOps {
     static constexpr bool HB = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_POS;
     static constexpr bool HX = EPI == EPI_BIAS_RES || EPI == EPI_RES || EPI == EPI_BIAS_POS;
-    static constexpr bool HL = EPI == EPI_LNB || EPI == EPI_LNB_GELU;
     float bv[HB ? TN : 1];
     float xv[HX ? TM : 1][HX ? TN : 1][4];
-    float c0[HL ? TN : 1], c1[HL ? TN : 1];         // LayerNorm fold: per column
-    float mu[HL ? TM : 1][4], rs[HL ? TM : 1][4];  // per row
 };
 
 template <int EPI, int TM, int TN>
@@ -90,24 +82,6 @@ __device__ __forceinline__ void epi_load(const EpiArgs& ea, int M, int N, int mb
         const int n = nb + j * 16 + (lane & 15);
         ncl[j] = n < N ? n : N - 1;
         if constexpr (E::HB) e.bv[j] = bf2f(ea.bias[ncl[j]]);
-        if constexpr (E::HL) {
-            e.c0[j] = ea.lnc0[ncl[j]];
-            e.c1[j] = ea.lnc1[ncl[j]];
-        }
-    }
-    if constexpr (E::HL) {
-        if (!ea.lnst) {  // (segment records: k_gemm_p's prologue fills mu / rs from LDS)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int m = mb + i * 16 + (lane >> 4) * 4 + r;
-                    m = m < M ? m : M - 1;
-                    const float2 v = *reinterpret_cast<const float2*>(ea.lnmr + 2 * (long)m);
-                    e.mu[i][r] = v.x;
-                    e.rs[i][r] = v.y;
-                }
-        }
     }
     if constexpr (E::HX) {
 #pragma unroll
@@ -145,14 +119,6 @@ __device__ __forceinline__ void epi_apply(const EpiArgs& ea, int M, int N, int m
 #pragma unroll
                 for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(e.xv[i][j][r]));
     }
-    if constexpr (E::HL) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(e.c0[j]), "+v"(e.c1[j]));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(e.mu[i][r]), "+v"(e.rs[i][r]));
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -170,9 +136,6 @@ __device__ __forceinline__ void epi_apply(const EpiArgs& ea, int M, int N, int m
                 else if constexpr (EPI == EPI_RES) o = rbf(a) + e.xv[i][j][r];
                 else if constexpr (EPI == EPI_BIAS_POS) o = rbf(a + e.bv[j]) + e.xv[i][j][r];
                 else if constexpr (EPI == EPI_GEGLU) o = rbf(gelu_tanh(rbf(a))) * rbf(acc2[i][j][r]);
-                else if constexpr (EPI == EPI_LNB) o = e.rs[i][r] * (a - e.mu[i][r] * e.c1[j]) + e.c0[j];
-                else if constexpr (EPI == EPI_LNB_GELU)
-                    o = gelu_tanh(rbf(e.rs[i][r] * (a - e.mu[i][r] * e.c1[j]) + e.c0[j]));
                 if (m < M && n < N) {
                     if constexpr (EPI == EPI_F32) ea.out_f32[(long)m * ea.ldo + n] = rbf(a);
                     else ea.out[(long)m * ea.ldo + n] = f2bf(o);
@@ -454,15 +417,14 @@ __device__ __forceinline__ void vm_wait_tiles(int n) {
 //
 // Round 4: when the grid splits into 8 equal blocks of bm row tiles x bn column tiles x bs K slices
 // (the host's xcd_block picks the shape that minimises the bytes each XCD must bring into its L2 --
-// bs/S of K x (bm row panels + bn weight panels) -- and passes it in the high bits of n_mt), XCD x
-// takes block x instead of a run: the batched prefill GEMMs otherwise read the whole activation panel
-// on every XCD (8-image down projection: 718 MB per launch fetched for ≈180 MB of operands).  Inside
-// a block the row tiles of one weight panel stay adjacent.
-__device__ __forceinline__ void xcd_tile(int n_mt_x, int& mt, int& nt, int& z) {
-    const int n_mt = n_mt_x & 1023, xb = (n_mt_x >> 10) & 0xFFFFF;  // (bit 30: k_gemm_w's weight policy)
-    const int S = gridDim.y;
-    const int G = gridDim.x * S;
-    const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+// bs/S of K x (bm row panels + bn weight panels) -- and passes it as `code`: bm | bn << 6 | bs << 14;
+// bit 30 is k_gemm_w's weight cache policy), XCD x takes block x instead of a run: the batched prefill
+// GEMMs otherwise read the whole activation panel on every XCD (8-image down projection: 718 MB per
+// launch fetched for ≈180 MB of operands).  Inside a block the row tiles of one weight panel stay adjacent.
+__host__ __device__ __forceinline__ void xcd_tile_of(int lin, int gx, int S, int n_mt, int code, int& mt, int& nt,
+                                                     int& z) {
+    const int xb = code & 0x3FFFF;
+    const int G = gx * S;
     const int x = lin & 7, j = lin >> 3;
     if (xb) {
         const int bm = xb & 63, bn = (xb >> 6) & 255, bs = xb >> 14;
@@ -482,204 +444,15 @@ __device__ __forceinline__ void xcd_tile(int n_mt_x, int& mt, int& nt, int& z) {
     nt = idx / (n_mt * S);
 }
 
-// gemm_res_ln's tail of a split-K k_gemm_p workgroup (its fp32 partial already stored write-through).
-// Per output tile the workgroup whose arrival count comes last reduces the S slabs in the fixed order
-// of k_splitk_res_norm (bitwise the same sum), adds bias and residual -> ea.out (bf16), and stores
-// per row and 32-column segment (sum, sum of squared deviations from the segment mean) of the bf16
-// result; per row tile the workgroup that completes the last tile combines the segments (Chan's
-// pairwise form, fixed order) into (mean, rstd) -> ea.lnmr.  Hand-offs per coh.h: write-through
-// stores, each storing wave drained, a barrier, one lane counts; the counting lane of the last
-// arrival resets the counter for the next launch.  S <= kResLnMaxSplit, N / 32 <= kResLnMaxSeg.
-constexpr int kResLnMaxSplit = 4, kResLnMaxSeg = kResLnSegs;
-template <int TM, int TN, int WN, int BM>
-__device__ __forceinline__ void res_ln_tail(const EpiArgs& ea, const float* __restrict__ ws, int M, int N, int mt,
-                                            int nt, int n_nt, int z, int wm, int wn, int lane,
-                                            const f32x4 (&acc)[TM][TN]) {
-    __shared__ int last_tile, last_rows;
-    const int tid = threadIdx.x;
-    const int S = gridDim.y;
-    constexpr int SEGW = TN * 16;
-    const int nseg = N / SEGW;
-    const int m0 = mt * BM + wm * TM * 16, n0 = nt * WN * SEGW + wn * SEGW;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* tc = ea.tcnt + (long)mt * n_nt + nt;
-    if (tid == 0) {
-        const bool l = __hip_atomic_fetch_add(tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)S;
-        if (l) __hip_atomic_store(tc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_tile = l;
-    }
-    __syncthreads();
-    if (!last_tile) return;
-    // every slab's value, the bias and the residual issued before any is used (rows past M clamped)
-    float v[kResLnMaxSplit][TM][TN][4];
-    float bv[TN], xv[TM][TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bv[j] = bf2f(ea.bias[n0 + j * 16 + (lane & 15)]);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-            m = m < M ? m : M - 1;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + j * 16 + (lane & 15);
-                xv[i][j][r] = bf2f(ea.res[(long)m * ea.ldr + n]);
-#pragma unroll
-                for (int q = 0; q < kResLnMaxSplit; ++q)
-                    v[q][i][j][r] = ldf_coh(ws + ((long)(q < S ? q : 0) * M + m) * N + n);
-            }
-        }
-    float x[TM][TN][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float a = z == 0 ? acc[i][j][r] : v[0][i][j][r];
-#pragma unroll
-                for (int q = 1; q < kResLnMaxSplit; ++q) {
-                    const float p = z == q ? acc[i][j][r] : v[q][i][j][r];
-                    a = q < S ? a + p : a;
-                }
-                const uint16_t o = f2bf(rbf(a + bv[j]) + xv[i][j][r]);
-                const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-                if (m < M) ea.out[(long)m * ea.ldo + n0 + j * 16 + (lane & 15)] = o;
-                x[i][j][r] = bf2f(o);
-            }
-    // segment statistics: the 16 lanes of one (lane >> 4) hold the segment's columns of 4 rows
-    const int seg = nt * WN + wn;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float sm = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) sm += x[i][j][r];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
-            const float mean = sm / (float)SEGW;
-            float d2 = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const float d = x[i][j][r] - mean;
-                d2 += d * d;
-            }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
-            const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-            if ((lane & 15) == 0 && m < M) {
-                stf_coh(ea.lnst + ((long)m * nseg + seg) * 2, sm);
-                stf_coh(ea.lnst + ((long)m * nseg + seg) * 2 + 1, d2);
-            }
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        unsigned* rc = ea.rcnt + mt;
-        const bool l = __hip_atomic_fetch_add(rc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == (unsigned)n_nt;
-        if (l) __hip_atomic_store(rc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_rows = l;
-    }
-    __syncthreads();
-    if (!last_rows || tid >= BM) return;
-    const int m = mt * BM + tid;
-    if (m >= M) return;
-    float sv[kResLnMaxSeg], dv[kResLnMaxSeg];
-#pragma unroll
-    for (int g = 0; g < kResLnMaxSeg; ++g) {
-        const int gc = g < nseg ? g : nseg - 1;
-        const unsigned long long w = __hip_atomic_load(
-            reinterpret_cast<const unsigned long long*>(ea.lnst + ((long)m * nseg + gc) * 2), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        sv[g] = __uint_as_float((unsigned)w);
-        dv[g] = __uint_as_float((unsigned)(w >> 32));
-    }
-    float tot = 0.f;
-#pragma unroll
-    for (int g = 0; g < kResLnMaxSeg; ++g) tot = g < nseg ? tot + sv[g] : tot;
-    const float mean = tot / (float)N;
-    float m2 = 0.f;
-#pragma unroll
-    for (int g = 0; g < kResLnMaxSeg; ++g) {
-        const float dm = sv[g] / (float)SEGW - mean;
-        m2 = g < nseg ? m2 + (dv[g] + (float)SEGW * dm * dm) : m2;
-    }
-    ea.lnmr[2 * (long)m] = mean;
-    ea.lnmr[2 * (long)m + 1] = 1.0f / sqrtf(m2 / (float)N + ea.ln_eps);
-}
-
-// gemm_res_stats epilogue: per row and 32-column segment of the bf16 result (the wave's TN x 16
-// columns of 4 rows per lane group), (sum, sum of squared deviations from the segment mean), plain stores
-template <int TM, int TN>
-__device__ __forceinline__ void seg_stats(const EpiArgs& ea, int M, int N, int mb, int seg, int lane,
-                                          const EpiOps<EPI_BIAS_RES, TM, TN>& e, const f32x4 (&acc)[TM][TN]) {
-    constexpr int SEGW = TN * 16;
-    const int nseg = N / SEGW;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float x[TN], sm = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                x[j] = bf2f(f2bf(rbf(acc[i][j][r] + e.bv[j]) + e.xv[i][j][r]));  // the stored value
-                sm += x[j];
-            }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
-            const float mean = sm / (float)SEGW;
-            float d2 = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const float d = x[j] - mean;
-                d2 += d * d;
-            }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) d2 += __shfl_xor(d2, o, 64);
-            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
-            if ((lane & 15) == 0 && m < M)
-                *reinterpret_cast<float2*>(ea.lnst + ((long)m * nseg + seg) * 2) = make_float2(sm, d2);
-        }
-}
-
-// gemm_lnfold's prologue over segment records: thread t < BM combines row m0 + t's lnseg records (fixed
-// order, Chan's pairwise form) into (mean, rstd) in LDS
-template <int BM>
-__device__ __forceinline__ void ln_rows_prologue(const EpiArgs& ea, int M, int D, int m0, float* lds_mr) {
-    const int t = threadIdx.x;
-    if (t < BM) {
-        int m = m0 + t;
-        m = m < M ? m : M - 1;
-        const int nseg = ea.lnseg;
-        float2 v[kResLnSegs];
-#pragma unroll
-        for (int g = 0; g < kResLnSegs; ++g)
-            v[g] = *reinterpret_cast<const float2*>(ea.lnst + ((long)m * nseg + (g < nseg ? g : nseg - 1)) * 2);
-        float tot = 0.f;
-#pragma unroll
-        for (int g = 0; g < kResLnSegs; ++g) tot = g < nseg ? tot + v[g].x : tot;
-        const float mean = tot / (float)D;
-        const float segw = (float)(D / nseg);
-        float m2 = 0.f;
-#pragma unroll
-        for (int g = 0; g < kResLnSegs; ++g) {
-            const float dm = v[g].x / segw - mean;
-            m2 = g < nseg ? m2 + (v[g].y + segw * dm * dm) : m2;
-        }
-        lds_mr[2 * t] = mean;
-        lds_mr[2 * t + 1] = 1.0f / sqrtf(m2 / (float)D + ea.ln_eps);
-    }
-    __syncthreads();
+__device__ __forceinline__ void xcd_tile(int n_mt, int code, int& mt, int& nt, int& z) {
+    xcd_tile_of(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x, gridDim.y, n_mt, code, mt, nt, z);
 }
 
 template <int NW, int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                    int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
-                                                   int n_mt, int n_nt) {
+                                                   int n_mt, int code) {
     constexpr int WN = NW / WM;
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
@@ -697,7 +470,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     const int wm = wave / WN, wn = wave % WN;
     // tile coordinates: the row tiles of one weight panel on one XCD (xcd_tile)
     int mt, nt, z;
-    xcd_tile(n_mt, mt, nt, z);
+    xcd_tile(n_mt, code, mt, nt, z);
     const int m0 = mt * BM, n0 = nt * BN;
     const int nkt_total = (K + 63) / 64;
     const int kt0 = z * kt_per_split;
@@ -788,20 +561,6 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     // epilogue operands first (see epi_load): held in registers through the k loop
     const int epi_mb = m0 + wm * TM * 16, epi_nb = n0 + wn * TN * 16;
     EpiOps<EPI, TM, TN> epi_ops;
-    if constexpr (!SPLIT && (EPI == EPI_LNB || EPI == EPI_LNB_GELU)) {
-        __shared__ float ln_mr[2 * BM];
-        if (ea.lnst) {
-            ln_rows_prologue<BM>(ea, M, K, m0, ln_mr);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int lr = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
-                    epi_ops.mu[i][r] = ln_mr[2 * lr];
-                    epi_ops.rs[i][r] = ln_mr[2 * lr + 1];
-                }
-        }
-    }
     if constexpr (!SPLIT) epi_load<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops);
     RopeOps<EPI == EPI_ROPE ? TM : 1> rope_ops;
     if constexpr (!SPLIT && EPI == EPI_ROPE) rope_load<TM, BN>(ea, M, epi_mb, epi_nb, lane, rope_ops);
@@ -851,7 +610,6 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 
     // C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + r
     if constexpr (SPLIT) {
-        const bool fused = ea.tcnt != nullptr;  // gemm_res_ln: partials write-through, reduced below
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -860,20 +618,13 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) {
-                        if (fused) stf_coh(ws + ((long)z * M + m) * N + n, acc[0][i][j][r]);
-                        else ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
-                    }
+                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
                 }
             }
-        if constexpr (NB == 1 && EPI == EPI_BIAS_RES)
-            if (fused) res_ln_tail<TM, TN, WN, BM>(ea, ws, M, N, mt, nt, n_nt, z, wm, wn, lane, acc[0]);
     } else if constexpr (EPI == EPI_ROPE) {
         rope_apply<TM>(ea, M, epi_mb, lane, rope_ops, acc[0]);
     } else {
         epi_apply<EPI, TM, TN>(ea, M, N, epi_mb, epi_nb, lane, epi_ops, acc[0], acc[NB - 1]);
-        if constexpr (EPI == EPI_BIAS_RES && NB == 1)
-            if (ea.lnst) seg_stats<TM, TN>(ea, M, N, epi_mb, nt * WN + wn, lane, epi_ops, acc[0]);
     }
 }
 
@@ -889,7 +640,7 @@ template <int NW, int WM, int TM, int TN, int NB, int ST, int LW, int EPI, bool 
 __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __restrict__ A, int lda,
                                                           const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                           int kt_per_split, EpiArgs ea, float* __restrict__ ws,
-                                                          long up_off, int n_mt, int n_nt) {
+                                                          long up_off, int n_mt, int code) {
     constexpr int WN = NW / WM;
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
@@ -903,7 +654,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int mt, nt, z;
-    xcd_tile(n_mt, mt, nt, z);
+    xcd_tile(n_mt, code, mt, nt, z);
     const int m0 = mt * BM, n0 = nt * BN;
     const int nkt_total = (K + 63) / 64;
     const int kt0 = z * kt_per_split;
@@ -943,11 +694,11 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
             src[i] = base + (long)row * ld + gk[i];
         }
         const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-        // one row tile (n_mt == 1, flagged in bit 30 of n_mt by launch_w): every weight byte is read by one
+        // one row tile (n_mt == 1, flagged in bit 30 of code by launch_w): every weight byte is read by one
         // workgroup once, so those pieces stream non-temporal; the activation panel, which every workgroup
         // re-reads, keeps the default policy.  Same box (tools/gpu_r4l.sh, the M = 288 gate|up): 43.1 / 43.8 /
         // 43.3 -> 41.2 / 41.7 / 41.4 us in situ, 224 px prefill 3.80 -> 3.77-3.79 ms
-        const bool wnt = (n_mt >> 30) & 1;
+        const bool wnt = (code >> 30) & 1;
         auto issue = [&](int kt, int slot) {
             const int kel = kt * 64;
             if (kel + 64 <= K) {
@@ -1117,7 +868,7 @@ template <int TM, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__ A, int lda,
                                                     const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                     int kt_per_split, EpiArgs ea, float* __restrict__ ws, long up_off,
-                                                    int n_mt) {
+                                                    int n_mt, int code) {
     static_assert(TM % 2 == 0, "row halves of whole 16-row tiles");
     constexpr bool DUAL = (EPI == EPI_GEGLU);
     constexpr int H = TM / 2;                 // row tiles per quadrant
@@ -1133,7 +884,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     int mt, nt, z;
-    xcd_tile(n_mt, mt, nt, z);
+    xcd_tile(n_mt, code, mt, nt, z);
     const int m0 = mt * BM, n0 = nt * (DUAL ? 128 : 256);
     const int nkt_total = K / 64;
     const int kt0 = z * kt_per_split;
@@ -1489,14 +1240,15 @@ size_t gemm_ws_bytes(int M, int N, int K) {
     return p.split > 1 ? (size_t)p.split * M * N * sizeof(float) : 0;
 }
 
-// host: the XCD block shape for xcd_tile (packed into n_mt's high bits), or 0 for the run order --
-// used only when it cuts the bytes the 8 XCDs must fetch into their L2s by at least 20 %
+// host: the XCD block shape for xcd_tile's `code` argument, or 0 for the run order -- used only when
+// it cuts the bytes the 8 XCDs must fetch into their L2s by at least 20 %.  Memoised per launch shape
+// behind a mutex (contexts may be driven from several host threads).
 static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K);
 static int xcd_block(int n_mt, int n_nt, int S, int BM, int BN, int K) {
-    static const bool off = [] { const char* e = getenv("PGMI_GEMM_XBLK"); return e && atoi(e) == 0; }();
-    if (off) return 0;
-    static std::map<std::tuple<int, int, int, int, int, int>, int> memo;  // (host-side, per launch shape)
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int, int, int>, int> memo;
     const auto key = std::make_tuple(n_mt, n_nt, S, BM, BN, K);
+    std::lock_guard<std::mutex> lock(mu);
     auto it = memo.find(key);
     if (it != memo.end()) return it->second;
     const int code = xcd_block_pick(n_mt, n_nt, S, BM, BN, K);
@@ -1510,7 +1262,7 @@ static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
     // 224 px tower 1.46 -> 1.53 ms (its split-K fc2 picked a block order that reads fewer bytes and
     // runs slower): the block order is used for the batched prefills' activation panels (>= 2048 rows)
     if ((long)n_mt * BM < 2048) return 0;
-    if (G % 8 != 0 || n_mt >= 1024 || G > 65536) return 0;
+    if (G % 8 != 0 || n_mt >= 64 * 8 || G > 65536) return 0;
     const double ks = (double)K / S * 2.0;  // bytes per row of one K slice
     // the run order: XCD x reads the (mt, z) row panels and (nt, z) weight panels of its run
     const long q = G / 8;
@@ -1543,8 +1295,9 @@ static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
 
 // in-situ timing probe (pgmi_prefill_probe): when a pair of events is armed, the next GEMM kernel is
 // launched with hipExtLaunchKernelGGL, whose events take that kernel's own start and end -- a time
-// free of the host's launch pace and of the stream's other packets; the pair is used once
-static hipEvent_t g_probe_ev0 = nullptr, g_probe_ev1 = nullptr;
+// free of the host's launch pace and of the stream's other packets; the pair is used once.  Per host
+// thread: the engine arms the pair right before the GEMM call that takes it, on the same thread.
+static thread_local hipEvent_t g_probe_ev0 = nullptr, g_probe_ev1 = nullptr;
 void gemm_probe_events(hipEvent_t start, hipEvent_t stop) {
     g_probe_ev0 = start;
     g_probe_ev1 = stop;
@@ -1613,7 +1366,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
     dim3 grid(n_mt * n_nt, split);
-    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10);
+    const int code = xcd_block(n_mt, n_nt, split, BM, NB * BN, K);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>),
@@ -1624,7 +1377,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
     if (EPI < 0 || split > 1) {
         PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, true>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K, per,
-                           ea, ws, up_off, nmx, n_nt);
+                           ea, ws, up_off, n_mt, code);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1633,7 +1386,7 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         }
     } else {
         PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, NB, STQ, EK, false>), grid, dim3(64 * NW), lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, nmx, n_nt);
+                           per, ea, ws, up_off, n_mt, code);
     }
 }
 
@@ -1652,8 +1405,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
     dim3 grid(n_mt * n_nt, split);
-    static const bool wnt_off = [] { const char* e = getenv("PGMI_GEMM_WNT"); return e && atoi(e) == 0; }();
-    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, NB * BN, K) << 10) | (n_mt == 1 && !wnt_off ? 1 << 30 : 0);
+    const int code = xcd_block(n_mt, n_nt, split, BM, NB * BN, K) | (n_mt == 1 ? 1 << 30 : 0);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>),
@@ -1665,7 +1417,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const dim3 block(64 * (NW + LW));
     if (EPI < 0 || split > 1) {
         PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, nmx, n_nt);
+                           per, ea, ws, up_off, n_mt, code);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1674,7 +1426,7 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
         }
     } else {
         PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                           per, ea, ws, up_off, nmx, n_nt);
+                           per, ea, ws, up_off, n_mt, code);
     }
 }
 
@@ -1691,7 +1443,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
     const int per = (nkt + split - 1) / split;
     const int n_mt = (M + BM - 1) / BM, n_nt = (N + BNO - 1) / BNO;
     dim3 grid(n_mt * n_nt, split);
-    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, DUAL ? 2 * BNO : BNO, K) << 10);
+    const int code = xcd_block(n_mt, n_nt, split, BM, DUAL ? 2 * BNO : BNO, K);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_8p<TM, EK, false>),
@@ -1702,7 +1454,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
     }
     if (EPI < 0 || split > 1) {
         PGMI_GEMM_LAUNCH((k_gemm_8p<TM, EK, true>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
-                           up_off, nmx);
+                           up_off, n_mt, code);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
             long blocks = (total4 + 255) / 256;
@@ -1711,7 +1463,7 @@ static void launch_8p(hipStream_t s, const uint16_t* A, int lda, const uint16_t*
         }
     } else {
         PGMI_GEMM_LAUNCH((k_gemm_8p<TM, EK, false>), grid, dim3(512), lds, s, A, lda, W, ldw, M, N, K, per, ea, ws,
-                           up_off, nmx);
+                           up_off, n_mt, code);
     }
 }
 
@@ -1811,6 +1563,7 @@ int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, 
         case EPI_BIAS_POS: launch_e<EPI_BIAS_POS>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
         case EPI_F32: launch_e<EPI_F32>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
         case EPI_GEGLU: launch_e<EPI_GEGLU>(s, A, lda, W, ldw, M, N, K, ea, ws, p, up_off); break;
+        case EPI_ROPE: return 0;  // gemm_qkv_rope only
     }
     return 1;
 }
@@ -1844,71 +1597,13 @@ bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W,
     return true;
 }
 
-// gemm_res_ln launcher: the split-K k_gemm_p with the fused tail (no k_splitk_epi after it)
-template <int WM, int TM, int TN, int ST>
-static int launch_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
-                         const EpiArgs& ea, float* ws, int split, bool dry) {
-    constexpr int NW = 4, WN = NW / WM, BM = WM * TM * 16, BN = WN * TN * 16;
-    constexpr int STQ = (size_t)ST * (BM + BN) * 128 <= 163840 ? ST : ST - 1;
-    constexpr size_t lds = (size_t)STQ * (BM + BN) * 128;
-    const int n_mt = (M + BM - 1) / BM, n_nt = N / BN;
-    if (N % BN != 0 || N / (TN * 16) > kResLnMaxSeg || n_mt * n_nt > kResLnTiles || n_mt > kResLnRowTiles) return 0;
-    if (dry) return split;
-    const int nkt = (K + 63) / 64, per = (nkt + split - 1) / split;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_p<NW, WM, TM, TN, 1, STQ, EPI_BIAS_RES, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-    }
-    const int nmx = n_mt | (xcd_block(n_mt, n_nt, split, BM, BN, K) << 10);
-    PGMI_GEMM_LAUNCH((k_gemm_p<NW, WM, TM, TN, 1, STQ, EPI_BIAS_RES, true>), dim3(n_mt * n_nt, split), dim3(64 * NW), lds,
-                     s, A, lda, W, K, M, N, K, per, ea, ws, 0L, nmx, n_nt);
-    return split;
-}
-
-int gemm_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K, const EpiArgs& ea,
-                float* ws, size_t ws_bytes, bool dry) {
-    const Plan p = choose(M, N, K, false);
-    const int nkt = (K + 63) / 64;
-    const int per = (nkt + p.split - 1) / p.split;
-    const int split = (nkt + per - 1) / per;  // every K range non-empty (as gemm)
-    if (split < 2 || split > kResLnMaxSplit || (size_t)split * M * N * sizeof(float) > ws_bytes) return 0;
-    if (!dry && (!ea.tcnt || !ea.rcnt || !ea.lnst || !ea.lnmr || !ea.bias || !ea.res || !ea.out)) return 0;
-    switch (p.cfg) {
-        case P64x64s4: return launch_res_ln<2, 2, 2, 4>(s, A, lda, W, M, N, K, ea, ws, split, dry);
-        case P96x64s4: return launch_res_ln<2, 3, 2, 4>(s, A, lda, W, M, N, K, ea, ws, split, dry);
-        default: return 0;
-    }
-}
-
-bool gemm_res_stats(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
-                    const EpiArgs& ea, bool dry) {
-    // P32x64s4 unsplit (the fastest unsplit out_proj of the round-3 sweep): 32-column segments
-    if (N % 64 != 0 || N / 32 > kResLnSegs) return false;
-    if (dry) return true;
-    launch_p<4, 2, 1, 2, 4, EPI_BIAS_RES>(s, A, lda, W, K, M, N, K, ea, nullptr, 1, 0);
-    return true;
-}
-
-bool gemm_lnfold(hipStream_t s, const uint16_t* A, int lda, const uint16_t* Wf, int M, int N, int K, bool gelu,
-                 const EpiArgs& ea, bool dry) {
-    const Plan p = choose(M, N, K, false);
-    if (p.split != 1) return false;
-    if (ea.lnst && (K % 32 != 0 || K / 32 != ea.lnseg || p.cfg != P96x64s4)) return false;  // BM <= 128 prologue
-#define F_(wm, tm, tn, st)                                                                                       \
-    do {                                                                                                         \
-        if (dry) break;                                                                                          \
-        if (gelu) launch_p<4, wm, tm, tn, st, EPI_LNB_GELU>(s, A, lda, Wf, K, M, N, K, ea, nullptr, 1, 0);       \
-        else launch_p<4, wm, tm, tn, st, EPI_LNB>(s, A, lda, Wf, K, M, N, K, ea, nullptr, 1, 0);                 \
-    } while (0)
-    switch (p.cfg) {
-        case P64x64s4: F_(2, 2, 2, 4); break;
-        case P96x64s4: F_(2, 3, 2, 4); break;
-        default: return false;
-    }
-#undef F_
-    return true;
+// host replica of a launch's tile order (pgmi_debug_gemm_tiles: the CPU test that every workgroup of the
+// grid gets a distinct (row tile, column tile, K slice)); returns the XCD block code the launch would use
+int gemm_tile_order(int n_mt, int n_nt, int S, int BM, int BN, int K, int* mt, int* nt, int* z) {
+    const int code = xcd_block(n_mt, n_nt, S, BM, BN, K);
+    const int gx = n_mt * n_nt;
+    for (int lin = 0; lin < gx * S; ++lin) xcd_tile_of(lin, gx, S, n_mt, code, mt[lin], nt[lin], z[lin]);
+    return code;
 }
 
 }  // namespace pgmi

@@ -104,10 +104,9 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
         gemv_mf_ores(s, a, o_out);
         return;
     }
-    // grid capped so each workgroup's combine prologue is amortised over 8 output rows (PGMI_ORES_CAP:
-    // probe knob for same-box sweeps of the cap)
-    static const int cap = [] { const char* e = getenv("PGMI_ORES_CAP"); return e ? atoi(e) : 256; }();
-    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, cap);
+    // grid capped so each workgroup's combine prologue is amortised over 8 output rows (256 / 128 / 64
+    // measured in round 4: 952 / 928-939 / 894-899 tok/s, profiles/r04_b1_probes_ab.txt)
+    if (B <= 1) launch_gemv<1, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 2) launch_gemv<2, 4, 2, GV_ORES>(s, a, 256);
     else if (B <= 4) launch_gemv<4, 4, 1, GV_ORES>(s, a, 256);
     else launch_gemv<8, 4, 1, GV_ORES>(s, a, 256);

@@ -743,26 +743,21 @@ void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
     else launch_mf<GV_QKV, 1, 256, 8, 1, true>(s, r, groups_of(r.n_units), 1, nullptr);  // input already normed
 }
 
-static int mf_gu_blocks() {
-    const char* e = getenv("PGMI_MF_GU_BLOCKS");  // probe knob (same-box sweeps of the unstaged form)
-    return e ? atoi(e) : 512;
-}
-
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
     // register-streamed MFMA form: 4 waves split K (512 each), 512 workgroups (2 per CU) dealing the
     // 1,024 row groups grid-stride, so each stages its 8 normalised rows for two groups; same-box A/B
     // (tools/b8_ab.sh) B = 8 step 1.737 -> 1.681 ms against the one-workgroup-per-CU LDS-DMA ring
     // (k_gemv_ml, 4 waves x 3-deep rings); 256 / 384 / 1,024 workgroups and 2 or 8 K-split waves
-    // measured slower (1.746-2.051 ms)
+    // measured slower (1.746-2.051 ms); the unstaged form re-swept in round 4 (profiles/r04_gu_blocks_ab.txt:
+    // 512 best against 384 / 768 / 1,024)
     if (a.norm_w) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
-    else launch_mf<GV_GEGLU, 2, 512, 4, 1, true>(s, a, mf_gu_blocks(), 1, nullptr);  // input already normed
+    else launch_mf<GV_GEGLU, 2, 512, 4, 1, true>(s, a, 512, 1, nullptr);  // input already normed
 }
 
 // o_proj: combine the attention partials once (-> o, bf16 [nb][K]), then the residual GEMV
 void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     const int K = a.K;
-    if (a.part)  // (nullptr: o was combined by the attention launch itself, attention_decode_comb)
-        hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 63) / 64), dim3(64), 0, s, a, o, K);
+    hipLaunchKernelGGL(k_attn_combine, dim3((a.nb * K / 8 + 63) / 64), dim3(64), 0, s, a, o, K);
     GemvArgs r = a;
     r.x = o;
     r.norm_w = nullptr;

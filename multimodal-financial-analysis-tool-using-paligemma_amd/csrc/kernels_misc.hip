@@ -462,47 +462,6 @@ void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* 
 #undef SRN_
 }
 
-// ---------------------------------------------------------------- LayerNorm fold (weights)
-// one workgroup per output row n; sums in fixed order (per-thread strided, then block_sum)
-__global__ void __launch_bounds__(256) k_ln_fold(const uint16_t* __restrict__ W, const uint16_t* __restrict__ gamma,
-                                                 const uint16_t* __restrict__ beta, const uint16_t* __restrict__ bias,
-                                                 int K, uint16_t* __restrict__ Wf, float* __restrict__ c1,
-                                                 float* __restrict__ c0) {
-    __shared__ float red[4];
-    const long n = blockIdx.x;
-    float s1 = 0.f, s0 = 0.f;
-    for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
-        const uint4 wv = ldg16(W + n * K + k), gv = ldg16(gamma + k), bv = ldg16(beta + k);
-        const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
-        const uint16_t* ge = reinterpret_cast<const uint16_t*>(&gv);
-        const uint16_t* be = reinterpret_cast<const uint16_t*>(&bv);
-        u16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            o.v[j] = f2bf(bf2f(we[j]) * bf2f(ge[j]));
-            s1 += bf2f(o.v[j]);
-            s0 += bf2f(be[j]) * bf2f(we[j]);
-        }
-        *reinterpret_cast<u16x8*>(Wf + n * K + k) = o;
-    }
-    s1 = block_sum<256>(s1, red);
-    __syncthreads();
-    s0 = block_sum<256>(s0, red);
-    if (threadIdx.x == 0) {
-        c1[n] = s1;
-        c0[n] = s0 + bf2f(bias[n]);
-    }
-}
-
-void ln_fold_weights(hipStream_t s, const uint16_t* W, const uint16_t* gamma, const uint16_t* beta,
-                     const uint16_t* bias, int N, int K, uint16_t* Wf, float* c1, float* c0) {
-    if (K % 8 != 0) {
-        fprintf(stderr, "pgmi: ln_fold_weights: K %d %% 8 != 0\n", K);
-        std::abort();
-    }
-    hipLaunchKernelGGL(k_ln_fold, dim3(N), dim3(256), 0, s, W, gamma, beta, bias, K, Wf, c1, c0);
-}
-
 // ---------------------------------------------------------------- patch im2col
 // out[(b*gh + i)*gw + j][c*P*P + kh*P + kw] = bf16(px[b][c][i*P+kh][j*P+kw]); zero pad to Kpad
 __global__ void k_patchify(const void* __restrict__ px, int is_f32, int C, int H, int W, int P, int Kpad,

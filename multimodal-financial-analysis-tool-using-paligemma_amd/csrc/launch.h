@@ -17,8 +17,6 @@ enum Epi : int {
     EPI_GEGLU = 7,      // out = bf16(bf16(gelu(bf16(acc_gate))) * bf16(acc_up))  (dual B)
     EPI_ROPE = 8,       // Gemma q|k|v rows: RoPE on q and k, q -> q_out, k / v appended to the KV cache
                         // (modeling_gemma.py:197-198,259); gemm_qkv_rope only
-    EPI_LNB = 9,        // LayerNorm folded in (gemm_lnfold): out = bf16(r_m (acc - mu_m c1_n) + c0_n)
-    EPI_LNB_GELU = 10,  // out = bf16(gelu(bf16(r_m (acc - mu_m c1_n) + c0_n)))
 };
 
 struct EpiArgs {
@@ -44,19 +42,6 @@ struct EpiArgs {
     int L = 1;
     int nh = 0;
     int nkv = 0;
-    // gemm_res_ln (split-K reduced by the last-arriving workgroup of each tile, + bias + residual, and
-    // the per-row LayerNorm statistics of the result) and gemm_lnfold (that LayerNorm applied by the
-    // next projection's epilogue)
-    unsigned* tcnt = nullptr;       // per output tile arrival counter (zeroed; the last arriver resets it)
-    unsigned* rcnt = nullptr;       // per row tile: tiles finished
-    float* lnst = nullptr;          // [M][N / 32][2] per-row 32-column segment (sum, sum of squared deviations)
-    float* lnmr = nullptr;          // [M][2] (mean, 1 / sqrt(var + eps)) of the rows gemm_res_ln wrote
-    float ln_eps = 0.f;
-    const float* lnc1 = nullptr;    // [N] sum_k W'[n][k]     (W' = bf16(W diag(gamma)))
-    const float* lnc0 = nullptr;    // [N] sum_k beta_k W[n][k] + bias[n]
-    // gemm_res_stats / gemm_lnfold with lnseg > 0: the rows' statistics as lnseg 32-column segment
-    // records in lnst (written by the producer's epilogue), combined by the consumer's prologue
-    int lnseg = 0;
 };
 
 // C[M,N] = A[M,K] (row-major, lda) x W[N,K]^T (row-major, ldw).  For EPI_GEGLU the
@@ -72,26 +57,12 @@ bool gemm_qkv_rope(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W,
 int gemm(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
          Epi epi, const EpiArgs& ea, float* ws, size_t ws_bytes, int up_offset_rows = 0, bool defer = false);
 size_t gemm_ws_bytes(int M, int N, int K);
-// SigLIP one-image plan (P64x64s4 / P96x64s4 tiles): the residual projection as split-K with the
-// reduction + bias + residual in the last-arriving workgroup of each output tile, writing ea.out and
-// the rows' LayerNorm (mean, rstd) to ea.lnmr (ea.tcnt / rcnt / lnst scratch); 0 = the shape's plan
-// has no such form (nothing launched), else the split used
-constexpr int kResLnTiles = 1024, kResLnRowTiles = 64, kResLnSegs = 48;  // counter / statistics capacity
-int gemm_res_ln(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
-                const EpiArgs& ea, float* ws, size_t ws_bytes, bool dry = false);
-// unsplit residual projection (EPI_BIAS_RES) whose epilogue also stores each row's 32-column segment
-// (sum, sum of squared deviations) of the bf16 result to ea.lnst (plain stores, no hand-off inside the
-// launch); false = no such form for the shape (nothing launched)
-bool gemm_res_stats(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int M, int N, int K,
-                    const EpiArgs& ea, bool dry = false);
-// LN(x) W^T + bias as r_m (x W'^T - mu_m c1) + c0 over the raw rows x (EPI_LNB / EPI_LNB_GELU);
-// false = no fold form for the shape's plan (nothing launched)
-bool gemm_lnfold(hipStream_t s, const uint16_t* A, int lda, const uint16_t* Wf, int M, int N, int K, bool gelu,
-                 const EpiArgs& ea, bool dry = false);
 void gemm_force_plan(int cfg, int split);  // cfg < 0: automatic
 int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split);  // cfg < 0: remove the override
 // probe: the next GEMM kernel launched takes these events as its own start / stop (hipExtLaunchKernelGGL)
 void gemm_probe_events(hipEvent_t start, hipEvent_t stop);
+// host replica of the panel / 8-phase GEMMs' workgroup -> tile order (CPU test); returns the XCD block code
+int gemm_tile_order(int n_mt, int n_nt, int S, int BM, int BN, int K, int* mt, int* nt, int* z);
 constexpr int kGemmCfgs = 38;              // tile configurations (kernels_gemm.hip Cfg)
 
 // ---------------------------------------------------------------- decode GEMV
@@ -173,11 +144,6 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a);
 void attention_decode(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
                       int max_chunks);
 constexpr int kAttnChunk = 64;
-// B >= 3: flash-decoding whose last-arriving chunk per row combines the row into a.o (bf16 [B][G*256]);
-// cnt: one counter per row (128-B stride), zero between launches (the last arriver re-arms it)
-bool attn_comb_fused(int B);
-void attention_decode_comb(hipStream_t s, const AttnArgs& a, const StepState* st, int launch_keys, float* part,
-                           int max_chunks, unsigned* cnt);
 constexpr int kAttnPartStride = 16 * 256 + 32;  // floats per (b, kv head, chunk) record
 size_t attention_decode_part_floats(int B, int n_kv, int max_chunks);
 int attention_prefill_max_keys(int head_dim);
@@ -212,10 +178,6 @@ void rope_rows(hipStream_t s, const uint16_t* x, const uint16_t* cs, const uint1
 void splitk_res_norm(hipStream_t s, const float* ws, int split, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                      const uint16_t* b, float eps, uint16_t* out, int rows, int D);
 void rmsnorm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, uint16_t* out, int rows, int D);
-// LayerNorm (gamma, beta) followed by a linear layer (W [N][K], bias) as one projection of the raw rows
-// (gemm_lnfold): Wf = bf16(W diag(gamma)), c1[n] = sum_k Wf[n][k], c0[n] = sum_k beta_k W[n][k] + bias[n] (fp32)
-void ln_fold_weights(hipStream_t s, const uint16_t* W, const uint16_t* gamma, const uint16_t* beta,
-                     const uint16_t* bias, int N, int K, uint16_t* Wf, float* c1, float* c0);
 void layernorm(hipStream_t s, const uint16_t* x, const uint16_t* w, const uint16_t* b, float eps, uint16_t* out,
                int rows, int D);
 void embed_rows(hipStream_t s, const int64_t* ids, int rows, const uint16_t* E, int D, float normalizer,

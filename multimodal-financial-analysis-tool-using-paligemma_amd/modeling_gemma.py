@@ -342,15 +342,39 @@ class GemmaForCausalLM(nn.Module):
     def forward(self, attention_mask: Optional[torch.Tensor] = None, position_ids: Optional[torch.LongTensor] = None,
                 inputs_embeds: Optional[torch.FloatTensor] = None, kv_cache: Optional[KVCache] = None, **kwargs) -> dict:
         """Gemma over merged embeddings (x bf16(sqrt(hidden)) inside), KV appended at
-        kv_cache.num_items(); attention spans the whole cache (the reference's zero mask)."""
+        kv_cache.num_items().  attention_mask is the additive mask every layer adds to its scores
+        (modeling_gemma.py:268-269, passed down at :370-377, :409-414) and, as there, must be given.
+        The all-zero mask the merge builds (:506-518) runs the fused engine (attention over the whole
+        cache); any other mask runs the per-layer module forwards, whose attention adds it
+        (pgmi_op_attention_ex), and the tied lm_head GEMM -- bf16 logits cast to fp32, as :416-418."""
         if inputs_embeds is None:
             raise ValueError("inputs_embeds must be provided")
-        eng = self._pgmi_engine()
+        assert attention_mask is not None                                  # modeling_gemma.py:268
         B, L = inputs_embeds.shape[:2]
         if position_ids is None:
             position_ids = torch.arange(L).unsqueeze(0)
+        if not torch.is_tensor(attention_mask) or bool((attention_mask != 0).any()):
+            return self._forward_masked(attention_mask, position_ids, inputs_embeds, kv_cache)
+        eng = self._pgmi_engine()
         pos = _positions_2d(position_ids, B, L)
         logits = _run_lm(eng, kv_cache, B, L, pos, embeds=inputs_embeds, logits_rows=kwargs.get("logits_rows", 0))
+        out = {"logits": logits}
+        if kv_cache is not None:
+            out["kv_cache"] = kv_cache
+        return out
+
+    def _forward_masked(self, attention_mask, position_ids, inputs_embeds, kv_cache):
+        """A non-zero additive mask (causal, padding): GemmaModel's module forwards (each layer's
+        GemmaAttention adds the mask to its scores, :269) and the lm_head, :409-418."""
+        if kv_cache is not None and kv_cache._slab is not None:
+            raise NotImplementedError("a KVCache filled by the fused path attends every cached key; a non-zero "
+                                      "attention mask needs a fresh KVCache() (filled through update())")
+        _check_tied(self)
+        dev = self.lm_head.weight.device
+        mask = torch.as_tensor(attention_mask, device=dev)
+        pos = torch.as_tensor(position_ids, device=dev)
+        h = self.model(attention_mask=mask, position_ids=pos, inputs_embeds=inputs_embeds.to(dev), kv_cache=kv_cache)
+        logits = _modules.linear(h, self.lm_head.weight).float()
         out = {"logits": logits}
         if kv_cache is not None:
             out["kv_cache"] = kv_cache

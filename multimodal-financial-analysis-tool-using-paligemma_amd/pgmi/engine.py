@@ -57,6 +57,7 @@ class Engine:
         c.max_batch, c.max_seq = max_batch, max_seq
         c.max_kv = max_kv if max_kv else self.cfgd["t_max_pos"]
         self.max_batch, self.max_seq, self.max_kv = max_batch, max_seq, c.max_kv
+        self.decode_split = 0
         h = ctypes.c_void_p()
         N.check(self.lib.pgmi_create(self.device.index, ctypes.byref(c), ctypes.byref(h)), "pgmi_create")
         self.ctx = h
@@ -340,10 +341,10 @@ class Engine:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
 
-    def set_vision_lnfold(self, on: int) -> None:
-        """SigLIP LayerNorm fold (one image): 1 both LayerNorms, 2 LayerNorm2 via out_proj segment statistics,
-        0 separate LayerNorm launches (default), -1 default."""
-        N.check(self.lib.pgmi_set_vision_lnfold(self.ctx, int(on)), "pgmi_set_vision_lnfold")
+    def set_decode_split(self, layers: int) -> None:
+        """Graphed decode step as two graphs (the head + `layers` layers, then the rest); 0 = one graph."""
+        N.check(self.lib.pgmi_set_decode_split(self.ctx, int(layers)), "pgmi_set_decode_split")
+        self.decode_split = int(layers)
 
     def set_decode_staged_norm(self, on: int) -> None:
         """Batched decode RMSNorm form: 0 once per row (default), 1 staged per projection, -1 default."""

@@ -553,15 +553,111 @@ def make_ablation(n_kv=64, n_nokv=48, small=False):
     print(name, "written")
 
 
+def make_nokv_fp32():
+    """fp32 truth for full_nokv_bf16.npz (configs[2]): the reference model in fp32, KV cache disabled
+    with the ablation's semantics (a full forward over prompt + generated tokens each step,
+    ablation_study_fixed.py:244-251), teacher-forced on the bf16 run's greedy tokens."""
+    g = np.load(os.path.join(HERE, "full_nokv_bf16.npz"))
+    cfg = W.full_config(224)
+    sidx = g["sample_idx"]
+    ids = g["ids"]
+    toks = g["tokens"].reshape(-1)
+    P = np.load(os.path.join(HERE, "pixels.npz"))
+    px = torch.from_numpy(pixels_from_u8(P["u8_0_224"])[None])
+    model, _ = build_model(cfg, torch.float32)
+    fl = []
+    t0 = time.time()
+    with torch.no_grad():
+        for t in range(len(toks)):
+            cur = torch.from_numpy(np.concatenate([ids, toks[None, :t]], 1))
+            out = model(input_ids=cur, pixel_values=px, attention_mask=torch.ones_like(cur), kv_cache=None)
+            fl.append(out["logits"][:, -1, :].float().numpy()[:, sidx])
+    fl = np.concatenate(fl, 0)
+    rel = np.linalg.norm(g["sample_vals"] - fl, axis=-1) / np.linalg.norm(fl, axis=-1)
+    print(f"no-kv fp32 teacher-forced {len(toks)} steps in {time.time() - t0:.1f}s; ref bf16 vs fp32 rel-L2 "
+          f"max {rel.max():.4f} mean {rel.mean():.4f}")
+    np.savez_compressed(os.path.join(HERE, "full_nokv_fp32.npz"), sample_idx=sidx, sample_vals=fl)
+
+
+def make_ablation_fp32():
+    """fp32 truth for both modes of full_ablation_bf16.npz: the paper's harness itself
+    (ablation_study_fixed.py run_inference, both load_model_simple patches) on the reference model in
+    fp32, teacher-forced on the bf16 run's tokens.  run_inference picks each token by argmax of
+    outputs["logits"][:, -1, :] (:226-229) and uses the logits for nothing else, so the spy records the
+    fp32 row and hands the harness a one-hot row at the bf16 token: the harness's own loop (re-feeds,
+    masks, positions, cache) then walks the bf16 token path."""
+    sys.path.insert(0, REF)
+    import ablation_study_fixed as AB
+    g = np.load(os.path.join(HERE, "full_ablation_bf16.npz"))
+    cfg = W.full_config(224)
+    sidx = g["sample_idx"]
+    ids = g["ids"]
+    model, _ = build_model(cfg, torch.float32)
+    model._merge_input_ids_with_image_features = types.MethodType(AB.patched_merge_input_ids_with_image_features, model)
+    for layer in model.language_model.model.layers:
+        layer.self_attn.rotary_emb.forward = types.MethodType(AB.patched_rotary_forward, layer.self_attn.rotary_emb)
+    tok = FakeTokenizer(ids, cfg["image_token_index"])
+    proc = RP.PaliGemmaProcessor(tok, W.num_image_tokens(cfg), cfg["vision_config"]["image_size"])
+    sync = torch.cuda.synchronize
+    torch.cuda.synchronize = lambda *a, **k: None
+    res = {"sample_idx": sidx}
+    try:
+        for mode in ("kv", "nokv"):
+            teacher = g[f"{mode}_tokens"].reshape(-1)
+            rows, picks = [], []
+            orig_forward = model.forward
+
+            def spy(*a, **k):
+                out = orig_forward(*a, **k)
+                last = out["logits"][:, -1, :].detach().float()
+                rows.append(last.numpy()[:, sidx].copy())
+                picks.append(int(last.argmax()))
+                step = len(rows) - 2                     # rows[0] is the discarded prefill
+                if step >= 0:
+                    forced = torch.zeros_like(out["logits"][:, -1:, :])
+                    forced[..., int(teacher[step])] = 1.0
+                    out = dict(out)
+                    out["logits"] = forced
+                return out
+
+            model.forward = spy
+            t0 = time.time()
+            try:
+                with torch.no_grad():
+                    r = AB.run_inference(model, proc, COCO[0], "p",
+                                         {"dtype": torch.float32, "kv_cache": mode == "kv", "max_tokens": len(teacher),
+                                          "temperature": 0.0}, return_tokens=True)
+            finally:
+                del model.forward
+            assert np.array_equal(np.array(r["token_ids"]).reshape(-1), teacher)
+            fl = np.concatenate(rows[1:], 0)
+            rel = np.linalg.norm(g[f"{mode}_sample_vals"] - fl, axis=-1) / np.linalg.norm(fl, axis=-1)
+            agree = int((np.array(picks[1:]) == teacher).sum())
+            print(f"ablation fp32 {mode}: {len(teacher)} steps in {time.time() - t0:.1f}s, fp32 argmax == bf16 "
+                  f"token at {agree}/{len(teacher)}; ref bf16 vs fp32 rel-L2 max {rel.max():.4f} mean {rel.mean():.4f}")
+            res[f"{mode}_sample_vals"] = fl
+    finally:
+        torch.cuda.synchronize = sync
+    np.savez_compressed(os.path.join(HERE, "full_ablation_fp32.npz"), **res)
+    print("full_ablation_fp32.npz written")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation", "448decode"], default=None,
+    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation", "448decode", "r5"], default=None,
                     help="generate only one later round's fixtures (full_batch8 / full256 / full_ablation)")
     a = ap.parse_args()
     torch.set_num_threads(8)
-    px = make_pixels() if a.only not in ("batch8", "batch8_fp32", "ablation") else None
-    if a.only == "batch8":
+    px = make_pixels() if a.only not in ("batch8", "batch8_fp32", "ablation", "r5") else None
+    if a.only == "r5":
+        # round 5: fp32 truths for configs[2] (no-KV) and both modes of the ablation harness; configs[3]'s
+        # batched rows at their stated 256 output tokens, with their fp32 truths
+        make_nokv_fp32()
+        make_ablation_fp32()
+        make_batch_images(n_tokens=256)
+        make_batch_fp32()
+    elif a.only == "batch8":
         make_batch_images()
         make_batch_fp32()
     elif a.only == "batch8_fp32":

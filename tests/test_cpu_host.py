@@ -30,6 +30,34 @@ def test_library_exports_every_declared_symbol():
     assert lib.pgmi_version().startswith(b"pgmi")
 
 
+@pytest.mark.parametrize("n_mt,n_nt,S,BM,BN,K,blocked", [
+    (8, 16, 2, 288, 128, 16384, True),     # 8-image text down (W288w split 2): the XCD block raster
+    (8, 9, 2, 288, 128, 4304, None),       # 8-image vision fc2
+    (9, 128, 1, 256, 256, 2048, None),     # 8-image gate|up (E256, dual)
+    (6, 8, 5, 192, 256, 16384, False),     # 448 px down (E192 split 5): below the 2,048-row panel bound
+    (1, 128, 1, 288, 128, 2048, False),    # 224 px gate|up (W288n, one row tile)
+    (3, 16, 4, 128, 128, 16384, False),    # 224 px down (W128x128 split 4)
+    (4, 18, 1, 64, 64, 1152, False),       # vision out_proj (P64x64s4)
+    (2048, 3, 1, 128, 128, 2048, False),   # M = 262,144 rows: n_mt past the old 10-bit packing
+    (7, 5, 3, 64, 64, 640, False),         # a grid that is not a multiple of 8
+])
+def test_gemm_tile_order_is_a_permutation(n_mt, n_nt, S, BM, BN, K, blocked):
+    """Every workgroup of a panel / 8-phase GEMM grid gets a distinct (row tile, column tile, K slice)
+    (kernels_gemm.hip xcd_tile, its host replica): the XCD block raster and the run order are both
+    permutations of the tile set, at every row-tile count (the block code travels in its own argument)."""
+    from pgmi import _native as N
+    lib = N.lib()
+    G = n_mt * n_nt * S
+    mt, nt, z = (np.zeros(G, np.int32) for _ in range(3))
+    code = lib.pgmi_debug_gemm_tiles(n_mt, n_nt, S, BM, BN, K, mt.ctypes.data, nt.ctypes.data, z.ctypes.data)
+    assert code >= 0
+    if blocked is not None:
+        assert (code != 0) == blocked, code
+    assert mt.min() >= 0 and mt.max() < n_mt and nt.min() >= 0 and nt.max() < n_nt and z.min() >= 0 and z.max() < S
+    flat = (mt.astype(np.int64) * n_nt + nt) * S + z
+    assert np.array_equal(np.sort(flat), np.arange(G))
+
+
 def test_create_validates_config_without_gpu():
     """pgmi_create only builds the weight layout (no device memory): it runs here."""
     from pgmi import _native as N

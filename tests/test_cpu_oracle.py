@@ -198,12 +198,18 @@ def test_batch8_fp32_fixture_consistency(golden_dir):
     row's reference-bf16 error vs its truth is in the range the bf16 model shows on image 0."""
     b8 = np.load(os.path.join(golden_dir, "full_batch8_bf16.npz"))
     f8 = np.load(os.path.join(golden_dir, "full_batch8_fp32.npz"))
-    f0 = np.load(os.path.join(golden_dir, "full_fp32.npz"))
+    n = f8["sample_vals"].shape[1]
+    assert n == b8["tokens"].shape[1] == 256          # configs[3]: 256 output tokens per image
+    # row 0 is image 0 with the prompt of full256_*: the same reference run, token for token
+    b0 = np.load(os.path.join(golden_dir, "full256_bf16.npz"))
+    f0 = np.load(os.path.join(golden_dir, "full256_fp32.npz"))
+    assert np.array_equal(b8["tokens"][0], b0["tokens"].reshape(-1)[:n])
     assert np.array_equal(f8["sample_idx"], b8["sample_idx"])
     assert f8["sample_vals"].shape == b8["sample_vals"].shape
     col = {int(c): i for i, c in enumerate(f0["sample_idx"])}
     shared = [col[int(c)] for c in f8["sample_idx"]]
-    assert np.array_equal(f8["sample_vals"][0], f0["sample_vals"][:, shared])
+    assert np.array_equal(f8["sample_vals"][0], f0["sample_vals"][:n, shared])
+    assert np.array_equal(b8["sample_vals"][0], b0["sample_vals"][:n, shared])
     for r in range(f8["sample_vals"].shape[0]):
         e = np.mean([np.linalg.norm(b8["sample_vals"][r, t] - f8["sample_vals"][r, t]) /
                      np.linalg.norm(f8["sample_vals"][r, t]) for t in range(f8["sample_vals"].shape[1])])
@@ -223,3 +229,51 @@ def test_448_decode_fixture_consistency(golden_dir):
     assert f["sample_vals"].shape == b["sample_vals"].shape == (16, b["sample_idx"].shape[0])
     e = np.linalg.norm(b["sample_vals"] - f["sample_vals"], axis=1) / np.linalg.norm(f["sample_vals"], axis=1)
     assert 1e-3 < e.min() and e.max() < 2e-2, e
+
+
+def test_ablation_and_nokv_fp32_fixture_consistency(golden_dir):
+    """full_ablation_fp32.npz / full_nokv_fp32.npz (fp32 truths of configs[2] and of the ablation harness,
+    teacher-forced on the bf16 tokens): same columns and steps as their bf16 fixtures; the no-KV truth's
+    step 0 is the KV-cached truth's step 0 bit for bit (the same prefill); the reference bf16 sits 1e-3..3e-2
+    from the no-KV truth, and further (the harness's model.to(bf16) also casts the rotary inv_freq,
+    ablation_study_fixed.py:182) from the harness's truth."""
+    g = np.load(os.path.join(golden_dir, "full_ablation_bf16.npz"))
+    f = np.load(os.path.join(golden_dir, "full_ablation_fp32.npz"))
+    assert np.array_equal(g["sample_idx"], f["sample_idx"])
+    for mode in ("kv", "nokv"):
+        a, b = g[f"{mode}_sample_vals"], f[f"{mode}_sample_vals"]
+        assert a.shape == b.shape == (len(g[f"{mode}_tokens"]), len(g["sample_idx"]))
+        e = np.linalg.norm(a - b, axis=1) / np.linalg.norm(b, axis=1)
+        assert 1e-3 < e.min() and e.max() < 0.15, (mode, e.min(), e.max())
+    n = np.load(os.path.join(golden_dir, "full_nokv_bf16.npz"))
+    nf = np.load(os.path.join(golden_dir, "full_nokv_fp32.npz"))
+    f0 = np.load(os.path.join(golden_dir, "full_fp32.npz"))
+    assert nf["sample_vals"].shape == n["sample_vals"].shape
+    assert np.array_equal(nf["sample_vals"][0], f0["sample_vals"][0])
+    e = np.linalg.norm(n["sample_vals"] - nf["sample_vals"], axis=1) / np.linalg.norm(nf["sample_vals"], axis=1)
+    assert 1e-3 < e.min() and e.max() < 3e-2, e
+
+
+def test_torch_cpu_decoder_matches_oracle():
+    """oracle/torch_cpu.py (the bench's CPU baseline, a torch bf16 port of the decode step) against the numpy
+    oracle on the same synthetic weights and the same cache: logits rel-L2 < 1e-2 and equal argmax over
+    three greedy steps (both keep the reference's bf16 rounding points; only accumulation order differs)."""
+    import torch
+    from oracle.torch_cpu import TorchCpuDecoder
+    cfg = W.small_config(vision_layers=1, text_layers=2, vocab=4096)
+    seed, n = 5, 40
+    P = W.synthetic_state_dict_f32(cfg, seed)
+    dec = TorchCpuDecoder(cfg, seed, max_kv=64)
+    dec.fill_cache(n)
+    kv = O.KV()
+    for i in range(2):
+        kv.update(dec.K[i, :n].float().numpy().transpose(1, 0, 2)[None], dec.V[i, :n].float().numpy().transpose(1, 0, 2)[None], i)
+    tok = 108
+    for s in range(3):
+        got = dec.step(tok, n + 1 + s).numpy()
+        ref = O.paligemma_decode(P, cfg, np.array([tok]), kv, n + 1 + s)[0, -1]
+        rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+        assert rel < 1e-2, (s, rel)
+        assert int(got.argmax()) == int(ref.argmax())
+        tok = int(ref.argmax())
+    assert torch.equal(dec.K[0, n:n + 3].float(), torch.from_numpy(kv.k[0][0, :, n:n + 3].transpose(1, 0, 2)))

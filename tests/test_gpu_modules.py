@@ -250,5 +250,53 @@ def test_gemma_model_modules_equal_fused(setup):
     staged = lm.model(attention_mask=torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda"), position_ids=pos,
                       inputs_embeds=emb)
     staged_logits = (staged.float() @ lm.lm_head.weight.float().T).bfloat16().float()
-    fused = lm(attention_mask=torch.ones(B, L, device="cuda"), position_ids=pos, inputs_embeds=emb)["logits"]
+    # the reference's 4-D zero mask (the merge's, modeling_gemma.py:506-518): the fused engine
+    zero = torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda")
+    fused = lm(attention_mask=zero, position_ids=pos, inputs_embeds=emb)["logits"]
     assert rel_l2(np32(staged_logits), np32(fused)) < 1e-2
+    # the reference asserts a mask is given (modeling_gemma.py:268)
+    with pytest.raises(AssertionError):
+        lm(attention_mask=None, position_ids=pos, inputs_embeds=emb)
+
+
+@torch.no_grad()
+def test_gemma_causal_lm_honours_additive_mask(setup):
+    """GemmaForCausalLM.forward adds a non-zero attention mask in every layer, as the reference does
+    (modeling_gemma.py:268-269 via :370-377, :409-414): a causal mask against the oracle's Gemma forward
+    with the same mask (every row's logits), and visibly different from the zero-mask result; a
+    fused-path KVCache refuses it rather than ignoring it."""
+    import modeling_gemma as MG
+    cfg, P, _ = setup
+    gc = MG.GemmaConfig(**cfg["text_config"])
+    lm = MG.GemmaForCausalLM(gc)
+    with torch.no_grad():
+        for name, p in lm.named_parameters():
+            key = "language_model." + name
+            if key in P:
+                p.data = torch.from_numpy(P[key]).to("cuda", torch.bfloat16)
+    lm.tie_weights()
+    lm = lm.cuda()
+    B, L = 1, 40
+    embn = _x(np.random.default_rng(12), B, L, 2048) * 0.05
+    emb = torch.from_numpy(embn).cuda().bfloat16()
+    posn = np.broadcast_to(np.arange(L), (B, L)).copy()
+    pos = torch.from_numpy(posn).cuda()
+    cm = O.bf16(np.triu(np.full((L, L), -1e4, np.float32), 1))[None, None]
+    causal = torch.from_numpy(cm).to("cuda", torch.bfloat16)
+    got = lm(attention_mask=causal, position_ids=pos, inputs_embeds=emb)["logits"]
+    assert got.shape == (B, L, cfg["text_config"]["vocab_size"]) and got.dtype == torch.float32
+    ref = O.gemma_forward(P, cfg, embn, posn, O.KV(), mask=cm)
+    with O.fp32_truth():
+        truth = O.gemma_forward(P, cfg, embn, posn, O.KV(), mask=cm)
+    assert_within_floor("gemma_causal_lm/causal_mask", np32(got), ref, truth)
+    # row 0 attends only itself under the causal mask: not the zero-mask (bidirectional) result
+    zero = lm(attention_mask=torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda"), position_ids=pos,
+              inputs_embeds=emb)["logits"]
+    assert rel_l2(np32(got[:, 0]), np32(zero[:, 0])) > 5e-2
+    # a cache the fused path owns attends every cached key: a non-zero mask is refused, not ignored
+    kv = MG.KVCache()
+    lm(attention_mask=torch.zeros(B, 1, L, L, dtype=torch.bfloat16, device="cuda"), position_ids=pos,
+       inputs_embeds=emb, kv_cache=kv)
+    with pytest.raises(NotImplementedError):
+        lm(attention_mask=torch.full((B, 1, 1, L + 1), -1e4, dtype=torch.bfloat16, device="cuda"),
+           position_ids=torch.full((B, 1), L, device="cuda"), inputs_embeds=emb[:, :1], kv_cache=kv)

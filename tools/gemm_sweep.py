@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--cfgs", default="0,2,4,5,6,7,8,9,10,11")
     ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--all", action="store_true", help="print every (cfg, split) row, not the best five")
     ap.add_argument("--cold", action="store_true",
                     help="rotate over distinct weight copies (> 256 MiB in all) so every call reads its weights "
                          "from HBM, as the layer loop of a forward does")
@@ -111,6 +112,9 @@ def main():
         print(f"{name:12s} M={M} N={Nn} K={K}: auto {auto[0]:7.1f} us ({flops / auto[0] / 1e6:6.0f} TF) | " +
               ", ".join(f"c{c}/s{sp}: {t:6.1f} ({flops / t / 1e6:4.0f} TF, err {er:.1e})" for t, c, sp, er in best),
               flush=True)
+        if args.all:
+            for t, c, sp, er in sorted(rows[1:]):
+                print(f"   {name} c{c}/s{sp}: {t:7.1f} us ({flops / t / 1e6:5.0f} TF, err {er:.1e})", flush=True)
         bad = [(c, sp, er) for _, c, sp, er in rows if er > 2e-2]
         if bad:
             print(f"   MISMATCH {name}: {bad}", flush=True)

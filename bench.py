@@ -460,22 +460,16 @@ def time_api(cfg, dev, seed, tokens):
             torch.cuda.synchronize()
             return time.perf_counter() - t0, n
 
-        # the binding's submission form (pgmi/binding.py DROPIN_DECODE_SPLIT) and the alternatives beside it:
-        # one graph per step vs two (the step's head + k layers first), alternating, best of 3 each
-        default_split = eng.decode_split
-        split_ms = {}
-        for rep in range(3):
-            for k in (0, 1, 2, 4):
-                eng.set_decode_split(k)
-                dt, n = decode_run()
-                split_ms.setdefault(k, []).append(dt * 1e3 / n)
-        eng.set_decode_split(default_split)
-        dt, n = decode_run()
+        # the step on demand (no lookahead, pgmi/lookahead.py) beside the default, alternating, best of 2
+        m.pgmi_lookahead = False
+        d0 = min(decode_run()[0] for _ in range(2))
+        m.pgmi_lookahead = True
+        dt, n = min(decode_run() for _ in range(2))
+        res["decode_ms_per_token_no_lookahead"] = round(d0 * 1e3 / n, 4)
     res.update(decode_ms_per_token=round(dt * 1e3 / n, 4), decode_tok_s=round(n / dt, 1), tokens_timed=n,
-               decode_split=default_split,
-               decode_split_ms_per_token={str(k): round(min(v), 4) for k, v in split_ms.items()},
                semantics="inference.py:55-78 through the drop-in module: pixel_values re-passed, float mask column "
-                         "appended, argmax of logits[:, -1, :], .item() per token")
+                         "appended, argmax of logits[:, -1, :], .item() per token; the module's greedy lookahead "
+                         "(pgmi/lookahead.py) runs each next step ahead of the caller")
     res["ablation_harness"] = time_ablation(m, ids0, px, tokens)
     del m, eng
     torch.cuda.empty_cache()

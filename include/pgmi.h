@@ -162,13 +162,6 @@ int pgmi_set_prefill_graph(pgmi_ctx* ctx, int on);
  * -1 = back to the default.  Same arithmetic either way (bf16 normalised rows);
  * drops captured decode graphs.  A tuning / test switch, no reference counterpart. */
 int pgmi_set_decode_staged_norm(pgmi_ctx* ctx, int on);
-/* Submission form of the graphed decode step (pgmi_decode*, use_graph != 0): layers > 0 captures the step
- * as two graphs -- the head (embedding, first norm) with the first `layers` layers, then the other layers
- * with the final norm, lm_head and argmax -- launched back to back, so the GPU starts after a short first
- * submission while the host still submits the second (a caller that waits on every token, inference.py:68's
- * .item(), hides most of the submission); 0 = one graph (default).  The same kernels in the same order:
- * outputs are bit-identical.  Drops captured decode graphs.  A tuning switch, no reference counterpart. */
-int pgmi_set_decode_split(pgmi_ctx* ctx, int layers);
 /* lm_head + .float() of GemmaForCausalLM (modeling_gemma.py:417-418) over final-normed hidden
  * rows: logits (device fp32 [rows][vocab]) = fp32(bf16(normed . E^T)) with the tied embedding E.
  * Together with pgmi_lm_final_hidden this materialises the prefill's all-row logits on demand

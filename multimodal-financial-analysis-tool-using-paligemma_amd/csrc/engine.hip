@@ -72,7 +72,6 @@ struct GraphKey {
 struct GraphEntry {
     int seen = 0;
     hipGraphExec_t exec = nullptr;
-    hipGraphExec_t exec2 = nullptr;  // the split submission's second graph (decode_split)
 };
 
 struct pgmi_ctx {
@@ -122,9 +121,6 @@ struct pgmi_ctx {
     // addresses at run time), captured on the second such call
     bool prefill_graph = true;
     int mf_staged = -1;  // batched decode RMSNorm form (mf_staged()); -1 = default (unstaged)
-    // graphed decode step submitted as two graphs (pgmi_set_decode_split): the first holds the step's head and
-    // this many layers, so the GPU starts while the host still submits the rest; 0 = one graph
-    int decode_split = 0;
     // device step state as the last enqueued per-phase decode step leaves it (advanced in-graph)
     bool step_known = false;
     int step_kv = 0, step_pos = 0;
@@ -144,12 +140,10 @@ void clear_pgraphs(pgmi_ctx* x) {
     x->pgraphs.clear();
 }
 
-// the captured decode steps (one or two graphs each)
+// the captured decode steps
 void clear_dgraphs(pgmi_ctx* x) {
-    for (auto& kv : x->graphs) {
+    for (auto& kv : x->graphs)
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-        if (kv.second.exec2) (void)hipGraphExecDestroy(kv.second.exec2);
-    }
     x->graphs.clear();
 }
 
@@ -941,14 +935,10 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
 // (kernels_gemv_mfma.hip PGMI_MF_NT) the unstaged form wins, same box: 1.4523 / 1.4550 -> 1.4330 / 1.4320 ms
 static bool mf_staged(const pgmi_ctx* x) { return x->mf_staged > 0; }
 
-// part: 0 = the whole step; 1 = its head (embedding / first norm and layers [0, decode_split)); 2 = the rest
-// (layers [decode_split, L), final norm, lm_head, argmax) -- the two graphs of the split submission
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr,
-                       int masked = 0, int part = 0) {
+                       int masked = 0) {
     const pgmi_config& c = x->c;
-    const int lsplit = std::min(std::max(x->decode_split, 1), c.t_layers - 1);
-    const int l_begin = part == 2 ? lsplit : 0, l_end = part == 1 ? lsplit : c.t_layers;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const float eps = c.t_rms_eps;
     const float normalizer = bf16_round_host(std::sqrt((float)H));
@@ -959,16 +949,14 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     const bool fold = !embeds && gemv_qkv_folds_embed(B) && c.t_layers > 0;
     const EmbedFold emb{ids, E, normalizer, c.pad_token_id, x->dH};
     // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
-    if (part != 2) {
-        if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
-        else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
-    }
+    if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
+    else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
     // B >= 3 (MFMA projections): every RMSNorm is computed once per row (k_rows_norm after o_proj, fused
     // into the down projection's combine for the next layer's input norm) and the q|k|v and gate|up
     // projections read the normalised rows dHn without staging
     const bool mf = B >= gemv_mf_min_batch() && !mf_staged(x);
-    if (mf && c.t_layers > 0 && part != 2) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
-    for (int i = l_begin; i < l_end; ++i) {
+    if (mf && c.t_layers > 0) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
+    for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
         gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
@@ -999,7 +987,6 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
                    c.t_intermediate, x->dACT);
         gemv_res(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws);
     }
-    if (part == 1) return 0;
     int nparts = 0;
     int64_t* nx = next_ids ? next_ids : x->d_next;
     // the step's last work also advances the device step state (pgmi_decode skips its host-side
@@ -1046,14 +1033,6 @@ int pgmi_set_decode_staged_norm(pgmi_ctx* x, int on) {
     if (!x) return fail(PGMI_E_ARG, "null context");
     x->mf_staged = on < 0 ? -1 : on != 0;
     clear_dgraphs(x);  // captured steps hold the other form's launches
-    return 0;
-}
-
-int pgmi_set_decode_split(pgmi_ctx* x, int layers) {
-    if (!x) return fail(PGMI_E_ARG, "null context");
-    if (layers < 0) return fail(PGMI_E_ARG, "layers must be >= 0");
-    x->decode_split = layers;
-    clear_dgraphs(x);  // captured steps hold the other submission form
     return 0;
 }
 
@@ -1137,19 +1116,15 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
             return 0;
         }
         HIPCHK(hipStreamSynchronize(s));
-        const bool two = x->decode_split > 0 && x->c.t_layers >= 2;
-        for (int p = two ? 1 : 0; p <= (two ? 2 : 0); ++p) {
-            hipGraph_t g;
-            HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-            rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked, p);
-            HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
-            if (rc) return rc;
-            HIPCHK(hipGraphInstantiate(p == 2 ? &ge.exec2 : &ge.exec, g, nullptr, nullptr, 0));
-            (void)hipGraphDestroy(g);
-        }
+        hipGraph_t g;
+        HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
+        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked);
+        HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
+        if (rc) return rc;
+        HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
     }
     HIPCHK(hipGraphLaunch(ge.exec, s));
-    if (ge.exec2) HIPCHK(hipGraphLaunch(ge.exec2, s));
     LAUNCHCHK();
     advanced();
     return 0;

@@ -29,6 +29,22 @@ namespace pgmi {
 constexpr int BK = 64;
 constexpr int LDSK = 72;  // padded row (elements)
 
+// Probe builds only (tools/build_variant.sh "-DPGMI_GEMM_DIAG=n"; never set in the product build): bit 0 = the
+// panel kernels' compute waves read their fragments but issue no MFMA, bit 1 = the LDS-DMA stages issue no
+// loads (the waits then pass at once) -- what the k-loop costs without the matrix work / without the intake
+#ifndef PGMI_GEMM_DIAG
+#define PGMI_GEMM_DIAG 0
+#endif
+template <int TM, int TN, int NB>
+__device__ __forceinline__ void diag_consume(const short8 (&fa)[TM], const short8 (&fb)[NB][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[b][j]));
+}
+
 template <int EPI>
 __device__ __forceinline__ void epi_store(const EpiArgs& ea, int m, int n, float acc, float acc2) {
     switch (EPI) {
@@ -514,6 +530,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 #define PGMI_LDS_AT(slot, i) ((__attribute__((address_space(3))) void*)(smem_p + (slot) * SBYTES + loff[i]))
     const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
     auto issue = [&](int kt, int slot) {
+        if constexpr (PGMI_GEMM_DIAG & 2) return;
         const int kel = kt * 64;
         if (kel + 64 <= K) {
 #pragma unroll
@@ -553,6 +570,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
     } while (0)
 #define PGMI_MFMAS(FA, FB)                                                                                  \
     do {                                                                                                    \
+        if constexpr (PGMI_GEMM_DIAG & 1) { diag_consume<TM, TN, NB>(FA, FB); break; }                      \
         _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) \
             _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) acc[b_][i_][j_] =                              \
                 mfma16(FA[i_], FB[b_][j_], acc[b_][i_][j_]);                                                \
@@ -700,6 +718,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
         // 43.3 -> 41.2 / 41.7 / 41.4 us in situ, 224 px prefill 3.80 -> 3.77-3.79 ms
         const bool wnt = (code >> 30) & 1;
         auto issue = [&](int kt, int slot) {
+            if constexpr (PGMI_GEMM_DIAG & 2) return;
             const int kel = kt * 64;
             if (kel + 64 <= K) {
 #pragma unroll
@@ -776,6 +795,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
     } while (0)
 #define PGMI_W_MFMA(FA, FB)                                                                                \
     do {                                                                                                   \
+        if constexpr (PGMI_GEMM_DIAG & 1) { diag_consume<TM, TN, NB>(FA, FB); break; }                     \
         _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int i_ = 0; i_ < TM; ++i_) \
             _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) acc[b_][i_][j_] =                             \
                 mfma16(FA[i_], FB[b_][j_], acc[b_][i_][j_]);                                               \
@@ -787,6 +807,11 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
     }
     for (int t = 0; t < nkt; ++t) {
         const uint8_t* sb = smem_w + slot * SBYTES;
+        // the kk=0 fragments (read behind the previous MFMA block) have landed: a real s_waitcnt (not asm), so
+        // the compiler's counter model knows nothing older is outstanding and does not drain the kk=1 reads
+        // below before the first MFMA (without it the loop-carried reads made it emit lgkmcnt(0) there, and
+        // the kk=1 fragment reads ran exposed instead of under the kk=0 MFMAs)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         PGMI_W_READ(fa1, fb1, sb, 1);
         __builtin_amdgcn_sched_barrier(0);
         PGMI_W_MFMA(fa0, fb0);
@@ -797,6 +822,11 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
             __builtin_amdgcn_s_barrier();        // tile t+1 is in slot `slot`
             __builtin_amdgcn_sched_barrier(0);
             PGMI_W_READ(fa0, fb0, smem_w + slot * SBYTES, 0);
+        } else {
+            // last tile: its kk=1 fragments must be in.  Waiting here (not at the join below) keeps the
+            // counter model exact on both paths, so the kk=1 MFMAs of the other tiles do not wait for the
+            // next tile's kk=0 reads issued after the barrier (the merged state made hipcc emit lgkmcnt(1))
+            __builtin_amdgcn_s_waitcnt(0xC07F);
         }
         __builtin_amdgcn_sched_barrier(0);
         PGMI_W_MFMA(fa1, fb1);
@@ -934,6 +964,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__
     }
 #define PGMI_8P_LDS(off) ((__attribute__((address_space(3))) void*)(sm8 + (off)))
     auto stageA = [&](int qa, int kt, int buf) {
+        if constexpr (PGMI_GEMM_DIAG & 2) return;
         kt = kt < kt1 ? kt : kt1 - 1;  // past the range: valid bytes into a buffer never read again
         const int kel = kt * 64;
         const int base = buf * TB + qa * HAB;
@@ -942,6 +973,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(sa[qa][i] + kel), PGMI_8P_LDS(base + la[i]), 16, 0, 0);
     };
     auto stageB = [&](int qb, int kt, int buf) {
+        if constexpr (PGMI_GEMM_DIAG & 2) return;
         kt = kt < kt1 ? kt : kt1 - 1;
         const int kel = kt * 64;
         const int base = buf * TB + 2 * HAB + qb * HBB;
@@ -979,6 +1011,13 @@ __global__ void __launch_bounds__(512, 1) k_gemm_8p(const uint16_t* __restrict__
     };
     auto mfmas = [&](auto qa_c, auto qb_c) {
         constexpr int QA = decltype(qa_c)::value, QB = decltype(qb_c)::value;
+        if constexpr (PGMI_GEMM_DIAG & 1) {
+#pragma unroll
+            for (int i = 0; i < H; ++i)
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) asm volatile("" ::"v"(fa[i][kk]), "v"(fb[QB][0][kk]), "v"(fb[QB][1][kk]));
+            return;
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll

@@ -31,6 +31,7 @@ from modeling_siglip import SiglipVisionConfig, SiglipVisionModel
 from pgmi import binding as _binding
 from pgmi import modules as _modules
 from pgmi.lazy_logits import LazyLogits
+from pgmi.lookahead import lookahead_for
 
 
 class KVCache:
@@ -481,6 +482,9 @@ class PaliGemmaForConditionalGeneration(nn.Module):
     # the reference's behaviour) or "last" (a (B, 1, V) tensor)
     pgmi_use_graph: bool = True
     pgmi_prefill_logits: str = "lazy"
+    # KV-cached decode steps run the greedy continuation one step ahead of the caller (pgmi/lookahead.py):
+    # bit-identical results, the host's per-token work overlaps the next step; off after two misses per cache
+    pgmi_lookahead: bool = True
 
     def __init__(self, config: PaliGemmaConfig):
         super().__init__()
@@ -631,10 +635,16 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             assert L == 1  # modeling_gemma.py:509
             position = int(attention_mask.shape[-1])  # cumsum of an all-ones mask, :526
             slab = kv_cache._ensure(eng, B, cache_len + 1)
-            logits = eng.decode(input_ids, slab, cache_len, position, logits=eng.logits_buffer(B),
-                                graph=self.pgmi_use_graph)
-            chk.launch()  # behind the step's launch: its host cost overlaps the step
-            logits = logits.clone().unsqueeze(1)
+            if self.pgmi_lookahead and self.pgmi_use_graph:
+                # the greedy continuation runs one step ahead of the caller (pgmi/lookahead.py); the padding
+                # check is enqueued behind the asked step and read before anything is committed
+                logits = lookahead_for(eng, B).step(kv_cache, slab, input_ids, cache_len, position, True,
+                                                    after_launch=chk.launch)
+            else:
+                logits = eng.decode(input_ids, slab, cache_len, position, logits=eng.logits_buffer(B),
+                                    graph=self.pgmi_use_graph)
+                chk.launch()  # behind the step's launch: its host cost overlaps the step
+                logits = logits.clone().unsqueeze(1)
             chk.wait()
             kv_cache._len = cache_len + 1
 

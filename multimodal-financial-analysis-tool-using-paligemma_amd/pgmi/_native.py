@@ -69,7 +69,6 @@ SIGNATURES = {
     "pgmi_decode_embeds_dev": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, i32, vp, i32, i64, vp, vp, i32, vp]),
     "pgmi_set_prefill_graph": (i32, [vp, i32]),
     "pgmi_set_decode_staged_norm": (i32, [vp, i32]),
-    "pgmi_set_decode_split": (i32, [vp, i32]),
     "pgmi_prefill_kernel": (i32, [vp, i32, i32, i32, vp]),
     "pgmi_debug_gemm_tiles": (i32, [i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "pgmi_prefill_probe": (i32, [vp, i32]),

@@ -18,7 +18,6 @@ from .engine import Engine
 
 # capacities of engines built by the Python API (pgmi_config.max_batch / max_seq / max_kv)
 DEFAULT_MAX_BATCH = 8
-DROPIN_DECODE_SPLIT = 2  # layers in the first of the decode step's two graphs (0 = one graph)
 DEFAULT_MAX_SEQ = 1472
 
 _DUMMY_TEXT = {"vocab_size": 8, "hidden_size": 2048, "intermediate_size": 16384, "num_hidden_layers": 0,
@@ -101,9 +100,6 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
             if p.dtype == torch.bfloat16 and p.device == dev:
                 p.data = view
     eng.prepare(inv_freq=inv_freq)
-    # the drop-in's callers wait on every token (inference.py:68 .item()): the graphed step is submitted as
-    # two graphs so the GPU starts after the short first one (pgmi_set_decode_split; bench.py dropin_api)
-    eng.set_decode_split(DROPIN_DECODE_SPLIT)
     module.__dict__["_pgmi_bound"] = _Bound(eng, _sample(module), inv_fp)
     return eng
 

@@ -57,7 +57,6 @@ class Engine:
         c.max_batch, c.max_seq = max_batch, max_seq
         c.max_kv = max_kv if max_kv else self.cfgd["t_max_pos"]
         self.max_batch, self.max_seq, self.max_kv = max_batch, max_seq, c.max_kv
-        self.decode_split = 0
         h = ctypes.c_void_p()
         N.check(self.lib.pgmi_create(self.device.index, ctypes.byref(c), ctypes.byref(h)), "pgmi_create")
         self.ctx = h
@@ -177,8 +176,13 @@ class Engine:
         return buf
 
     # ------------------------------------------------------------------ forward pieces
+    _stream_guard = None  # pgmi/lookahead.py: makes a call wait for a step still running on its side stream
+
     def _s(self):
-        return N.stream_handle(self.device)
+        h = N.stream_handle(self.device)
+        if self._stream_guard is not None:
+            self._stream_guard(h)
+        return h
 
     def _ready(self):
         if not self.prepared:
@@ -340,11 +344,6 @@ class Engine:
     def set_prefill_graph(self, on: bool) -> None:
         """Replay captured hipGraphs for repeated vision / language-model calls with the same buffers."""
         N.check(self.lib.pgmi_set_prefill_graph(self.ctx, int(bool(on))), "pgmi_set_prefill_graph")
-
-    def set_decode_split(self, layers: int) -> None:
-        """Graphed decode step as two graphs (the head + `layers` layers, then the rest); 0 = one graph."""
-        N.check(self.lib.pgmi_set_decode_split(self.ctx, int(layers)), "pgmi_set_decode_split")
-        self.decode_split = int(layers)
 
     def set_decode_staged_norm(self, on: int) -> None:
         """Batched decode RMSNorm form: 0 once per row (default), 1 staged per projection, -1 default."""

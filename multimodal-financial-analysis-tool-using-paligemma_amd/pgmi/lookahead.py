@@ -1,0 +1,126 @@
+"""Greedy lookahead for the drop-in decode loop (host runtime of the MI355X path; no reference counterpart).
+
+The reference's loop (inference.py:56-78) waits on every token: `next_token.item()` syncs the host, and
+only then does it build the next input and call forward() again.  Everything the host does between that
+sync and the next step's launch -- the loop's own ops, the forward call, the graph launch -- leaves the GPU
+idle (≈90 µs per token at the 3B shapes: bench.py dropin_api against the native step).
+
+GreedyLookahead runs the NEXT step before it is asked for, on a side stream: after the step the caller
+asked for, it enqueues the step whose input is that step's on-device argmax (torch.argmax semantics,
+written by the lm_head's last workgroup) into another logits buffer and the next KV row.  The caller's own
+ops (its argmax, `.item()`) stay on its stream and do not wait for it, so the GPU runs the next step while
+the host does its per-token work.  When the caller's next forward() brings that same token at the next
+position of the same cache, its stream waits for the lookahead (a GPU-side event), checks the token
+against the one the lookahead used, hands back the lookahead's logits and enqueues the following
+lookahead; the host waits only for the check.  Any other input (a sampled token, another position,
+another cache) runs the asked step on the caller's stream behind the lookahead, whose KV row lies past
+the cache's length and is overwritten.  After two misses in a row the lookahead stands down for that
+cache (a sampling loop, inference.py:64-66, would otherwise pay a wasted step per token).
+
+Ordering: the lookahead uses the engine's workspace and the cache's slab, so (1) the side stream waits for
+the caller's stream before every lookahead, (2) every later engine call on any other stream waits for the
+last lookahead (Engine._s() runs the guard installed here), and (3) the slab is marked as used by the side
+stream for the caching allocator.  Three ids / logits slots rotate, so the token check of one step never
+races the write of the step after it.  What the caller gets is bit-identical to the step run on demand:
+the same graphed step over the same inputs.
+"""
+from __future__ import annotations
+
+import weakref
+
+import torch
+
+NSLOT = 3
+
+
+class GreedyLookahead:
+    def __init__(self, eng, B: int):
+        self.eng, self.B = eng, B
+        V = eng.cfgd["t_vocab"]
+        dev = eng.device
+        # slot s: ids[s] is the input token of the step whose logits go to logits[s]; that step's argmax goes
+        # to ids[(s + 1) % NSLOT], the input of the step after it
+        self.logits = [torch.empty((B, V), dtype=torch.float32, device=dev) for _ in range(NSLOT)]
+        self.ids = [torch.zeros(B, dtype=torch.int64, device=dev) for _ in range(NSLOT)]
+        self.side = torch.cuda.Stream(device=dev)
+        self.flag = torch.zeros((), dtype=torch.bool).pin_memory()
+        self.ev_chk = torch.cuda.Event()
+        self.pending = None    # (weakref to the KVCache, kv_len, position, slot, event on the side stream)
+        self.last = None       # event of the last lookahead enqueued (what other streams must wait for)
+        self.hits = 0
+        eng._stream_guard = self._guard
+
+    def _guard(self, handle) -> None:
+        """Engine._s(): an engine call about to run on stream `handle` waits for the last lookahead."""
+        if self.last is not None and handle != self.side.cuda_stream:
+            torch.cuda.current_stream(self.eng.device).wait_event(self.last)
+
+    def _run(self, slab, kv_len, position, s, graph):
+        self.eng.decode(self.ids[s], slab, kv_len, position, logits=self.logits[s],
+                        next_ids=self.ids[(s + 1) % NSLOT], graph=graph)
+
+    def _ahead(self, kv_cache, slab, kv_len, position, s, graph):
+        """Enqueue on the side stream the step in slot s (its input ids[s]: the previous step's argmax)."""
+        if kv_len + 1 > slab.shape[3] or getattr(kv_cache, "_pgmi_misses", 0) >= 2:
+            self.pending = None
+            return
+        main = torch.cuda.current_stream(self.eng.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self.side.wait_event(ready)
+        with torch.cuda.stream(self.side):
+            self._run(slab, kv_len, position, s, graph)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        slab.record_stream(self.side)
+        self.last = ev
+        self.pending = (weakref.ref(kv_cache), kv_len, position, s, ev)
+
+    def step(self, kv_cache, slab, input_ids, cache_len: int, position: int, graph: bool, after_launch=None):
+        """The logits (B, 1, V) of the decode step for input_ids at KV row cache_len / rotary `position`
+        (a fresh tensor, as the reference returns); `after_launch` runs once the asked step is enqueued."""
+        main = torch.cuda.current_stream(self.eng.device)
+        ids = input_ids.reshape(-1).to(self.eng.device, torch.int64)
+        p = self.pending
+        self.pending = None
+        s = 0
+        if (p is not None and p[0]() is kv_cache and p[1] == cache_len and p[2] == position
+                and ids.numel() == self.B):
+            s = p[3]
+            main.wait_event(p[4])  # the lookahead in slot s has run: its logits and its input token are final
+            ne = torch.ne(ids, self.ids[s]).any()
+            self.flag.copy_(ne, non_blocking=True)
+            self.ev_chk.record(main)
+            out = self.logits[s].clone().unsqueeze(1)
+            if after_launch is not None:
+                after_launch()
+            # the next lookahead goes in before the host waits for the check: the GPU keeps running
+            self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph)
+            self.ev_chk.synchronize()
+            if not bool(self.flag):
+                kv_cache._pgmi_misses = 0
+                self.hits += 1
+                return out
+            # a miss (sampling, a forced token): the asked step runs on the caller's stream behind the
+            # lookahead just enqueued (Engine._s() makes it wait), over the same KV rows
+            kv_cache._pgmi_misses = getattr(kv_cache, "_pgmi_misses", 0) + 1
+            self.pending = None
+            s = (s + 2) % NSLOT
+        # the asked step on the caller's stream, behind any lookahead still in flight (it shares the slots,
+        # the engine's workspace and possibly this cache's rows)
+        if self.last is not None:
+            main.wait_event(self.last)
+        self.ids[s].copy_(ids)
+        self._run(slab, cache_len, position, s, graph)
+        out = self.logits[s].clone().unsqueeze(1)
+        if after_launch is not None:
+            after_launch()
+        self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph)
+        return out
+
+
+def lookahead_for(eng, B: int) -> GreedyLookahead:
+    la = getattr(eng, "_lookahead", None)
+    if la is None or la.B != B:
+        la = eng._lookahead = GreedyLookahead(eng, B)
+    return la

@@ -21,6 +21,7 @@ on the GPU (other float dtypes are rounded to bf16, as the fused path does).
 from __future__ import annotations
 
 import math
+from collections import OrderedDict
 
 import torch
 
@@ -28,17 +29,27 @@ from . import _native as N
 from .engine import Engine
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RES, EPI_RES, EPI_GEGLU = 0, 1, 2, 3, 4, 7
-_CTX = {}
+_CTX: "OrderedDict" = OrderedDict()
+_CTX_MAX = 8  # contexts kept (least recently used evicted): callers that make streams per call stay bounded
 
 
 def _ctx(device: torch.device) -> Engine:
     """Context for the single-op entries on (device, current stream): a zero-layer model whose scratch
     (split-K partials, patch-embedding staging, attention partials) is used from offset 0 by every op,
-    so ops issued on different streams get different contexts and never overwrite each other's."""
+    so ops issued on different streams get different contexts and never overwrite each other's.  At most
+    _CTX_MAX contexts are kept; an evicted one is freed once the device has drained."""
     dev = device.index if device.index is not None else torch.cuda.current_device()
     key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     e = _CTX.get(key)
+    if e is not None:
+        _CTX.move_to_end(key)
     if e is None:
+        while len(_CTX) >= _CTX_MAX:
+            (odev, _), old = _CTX.popitem(last=False)
+            # its scratch may still be read by kernels queued on its stream (which may itself be gone):
+            # drain the device before freeing (evictions are rare: one per stream past the bound)
+            torch.cuda.synchronize(odev)
+            del old
         from .binding import _DUMMY_TEXT, _DUMMY_VISION
         from .synthetic import init_policy
         cfg = {"vision_config": dict(_DUMMY_VISION), "text_config": dict(_DUMMY_TEXT), "image_token_index": 7,

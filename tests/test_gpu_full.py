@@ -85,35 +85,6 @@ def test_teacher_forced_64_steps(eng224, G):
     _teacher_forced(eng224, G, G["bf16"], G["fp32"], 64)
 
 
-@pytest.mark.parametrize("split", [1, 2, 17])
-@torch.no_grad()
-def test_decode_split_submission_bit_identical(eng224, G, split):
-    """The graphed decode step submitted as two graphs (pgmi_set_decode_split: the step's head + `split`
-    layers, then the rest; the drop-in binding's form) runs the same kernels in the same order: logits and
-    greedy tokens bit-identical to the one-graph step over 12 steps, and the step state advances the same."""
-    gb = G["bf16"]
-    ids = torch.from_numpy(gb["ids"]).cuda()
-    L = ids.shape[1]
-    feats = eng224.project(eng224.vision(_px(G, "u8_0_224")))
-    runs = []
-    for k in (0, split):
-        eng224.set_decode_split(k)
-        try:
-            kv = eng224.new_kv(1, 576)
-            lg = eng224.lm_forward(kv, 0, torch.arange(L)[None], ids=ids, image_feats=feats, logits_rows=1)[:, 0]
-            cur = lg.argmax(-1)
-            out = []
-            for t in range(1, 13):
-                step = eng224.decode(cur, kv, L + t - 1, L + t, graph=True).clone()
-                out.append(step)
-                cur = step.argmax(-1)
-            runs.append((torch.stack(out), kv.clone()))
-        finally:
-            eng224.set_decode_split(0)
-    assert torch.equal(runs[0][0], runs[1][0])
-    assert torch.equal(runs[0][1], runs[1][1])
-
-
 @torch.no_grad()
 def test_teacher_forced_256_steps(eng224, G):
     """configs[1] as BASELINE.json states it: 256 output tokens, KV length up to 544 (past the

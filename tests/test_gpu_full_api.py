@@ -125,3 +125,53 @@ def test_inference_loop_full_size(model, G):
     if len(diff):
         assert g["margin"][diff[0]] < 0.25, (diff[0], toks[:diff[0] + 2], ref[:diff[0] + 2])
     assert kv.num_items() == g["ids"].shape[1] + 63
+
+
+@torch.no_grad()
+def test_lookahead_bit_identical_greedy_and_forced(model, G):
+    """The greedy lookahead of the drop-in decode step (pgmi/lookahead.py, on by default) returns exactly
+    what the step run on demand returns: the inference.py loop for 24 tokens with the lookahead on and off,
+    logits bit for bit, once greedy (every lookahead used) and once with every third token forced to the
+    runner-up (a miss: the asked step runs behind the wasted lookahead, whose KV row is overwritten).  After
+    two misses in a row the lookahead stands down for that cache."""
+    import modeling_gemma as MG
+    from pgmi.lookahead import lookahead_for
+    g = G["64"]
+    ids0 = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+
+    def loop(lookahead, forced_every=0, n=24):
+        model.pgmi_lookahead = lookahead
+        try:
+            ids, mask, kv = ids0, torch.ones_like(ids0), MG.KVCache()
+            outs = []
+            for t in range(n):
+                out = model(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
+                lg = out["logits"][:, -1, :]
+                outs.append(lg.clone())
+                pick = 1 if forced_every and t % forced_every == forced_every - 1 else 0
+                nxt = torch.topk(lg, 2, dim=-1).indices[:, pick:pick + 1]
+                _ = int(nxt.item())
+                ids = nxt
+                mask = torch.cat([mask, torch.ones((1, 1), device=ids.device)], dim=-1)
+            return torch.cat(outs, 0), kv
+        finally:
+            model.pgmi_lookahead = True
+
+    eng = model._pgmi_engine()
+    for forced in (0, 3):
+        on, kv_on = loop(True, forced)
+        off, kv_off = loop(False, forced)
+        assert torch.equal(on, off), forced
+        n = kv_on.num_items()
+        assert n == kv_off.num_items() == ids0.shape[1] + 23
+        assert torch.equal(kv_on._slab[:, :, :, :n], kv_off._slab[:, :, :, :n])
+    la = lookahead_for(eng, 1)
+    hits = la.hits
+    # forced tokens on two steps in a row: the lookahead stands down for the cache
+    ids, mask, kv = ids0, torch.ones_like(ids0), MG.KVCache()
+    for t in range(8):
+        out = model(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
+        ids = torch.topk(out["logits"][:, -1, :], 2, dim=-1).indices[:, 1:2]
+        mask = torch.cat([mask, torch.ones((1, 1), device=ids.device)], dim=-1)
+    assert la.hits == hits and la.pending is None

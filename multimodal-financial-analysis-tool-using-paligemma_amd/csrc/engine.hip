@@ -102,6 +102,7 @@ struct pgmi_ctx {
     // decode workspace
     uint16_t *dH, *dQ, *dAO, *dACT;
     uint16_t* dHn;  // batched decode (B >= 3): the RMSNorm'd rows the unstaged MFMA projections read
+    float* dSS;     // batched decode: o_proj's 16-column partial sums of squares of h, [B][H / 16]
     float *opart, *pmax, *dlogits, *amax_v;
     int *pidx, *amax_i;
     int max_chunks;
@@ -601,6 +602,7 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->dAO, (size_t)B * H))) return rc;
         if ((rc = dalloc_t(x, &x->dACT, (size_t)B * c.t_intermediate))) return rc;
         if ((rc = dalloc_t(x, &x->dHn, (size_t)B * H))) return rc;
+        if ((rc = dalloc_t(x, &x->dSS, (size_t)B * (H / 16)))) return rc;
         x->max_chunks = (c.max_kv + 63) / 64;
         if ((rc = dalloc_t(x, &x->opart, attention_decode_part_floats(B, c.t_kv_heads, x->max_chunks)))) return rc;
         if ((rc = dalloc_t(x, &x->pmax, (size_t)B * gemv_logits_blocks()))) return rc;
@@ -928,9 +930,12 @@ static int lm_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, const void* i
     return 0;
 }
 
-// The batched form's RMSNorms: computed once per row (k_rows_norm / the down combine's fused norm) and read
-// unstaged by q|k|v and gate|up (default), or staged by each projection itself (pgmi_set_decode_staged_norm,
-// tested by test_batch_rows_teacher_forced_vs_own_reference[8-1]).  Equal
+// The batched form's RMSNorms: computed once per row -- the input norm by the down projection's combine for
+// the next layer (k_mf_combine_norm; q|k|v reads dHn unstaged), the post-attention norm from o_proj's 16-column
+// partial sums of squares, applied by gate|up as it loads h (default) -- or each projection stages and
+// normalises its rows itself (pgmi_set_decode_staged_norm,
+// tested by test_batch_rows_teacher_forced_vs_own_reference[8-1]).  Round 4, the unstaged form reading rows
+// normalised by separate passes against the staged form: equal
 // while the weight streams were non-temporal (B = 8 step 1.5449 vs 1.5452 ms); with the default cache policy
 // (kernels_gemv_mfma.hip PGMI_MF_NT) the unstaged form wins, same box: 1.4523 / 1.4550 -> 1.4330 / 1.4320 ms
 static bool mf_staged(const pgmi_ctx* x) { return x->mf_staged > 0; }
@@ -951,9 +956,12 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     // given input rows (a caller's merge, pgmi_decode_embeds): h = rows x bf16(sqrt(hidden)) (modeling_gemma.py:367-368)
     if (embeds) scale_rows(s, embeds, (long)B * H, normalizer, x->dH);
     else if (!fold) embed_rows(s, ids, B, E, H, normalizer, c.pad_token_id, x->dH);
-    // B >= 3 (MFMA projections): every RMSNorm is computed once per row (k_rows_norm after o_proj, fused
-    // into the down projection's combine for the next layer's input norm) and the q|k|v and gate|up
-    // projections read the normalised rows dHn without staging
+    // B >= 3 (MFMA projections): every RMSNorm is computed once per row -- the input norm fused into the
+    // down projection's combine for the next layer (q|k|v reads dHn unstaged), the post-attention norm's
+    // sums of squares written by o_proj's epilogue (dSS) and applied by gate|up as it loads h.  (Round 5,
+    // the input norm the same way -- the down combine writing partials, q|k|v normalising on load: q|k|v
+    // 5.97 -> 7.59 us for a combine no shorter, 4.63 -> 4.72 us; with the combine inside the down launch,
+    // B = 8 step 1.437 -> 1.446-1.465 ms, same box.)
     const bool mf = B >= gemv_mf_min_batch() && !mf_staged(x);
     if (mf && c.t_layers > 0) rows_norm(s, x->dH, TL(x, 0, "input_layernorm.weight"), eps, B, H, x->dHn);
     for (int i = 0; i < c.t_layers; ++i) {
@@ -975,10 +983,12 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         }
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                    B >= gemv_mf_min_batch() ? x->dAO : nullptr);
+                    B >= gemv_mf_min_batch() ? x->dAO : nullptr, mf ? x->dSS : nullptr);
         if (mf) {
-            rows_norm(s, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, B, H, x->dHn);
-            gemv_geglu(s, B, x->dHn, nullptr, eps, TL(x, i, "mlp.gate_proj.weight"), c.t_intermediate, x->dACT);
+            // the post-attention RMSNorm: its sums of squares come from o_proj's epilogue (dSS), gate|up
+            // normalises h on load (no k_rows_norm pass: B = 8 step -5 us per layer)
+            gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
+                       c.t_intermediate, x->dACT, x->dSS);
             gemv_res_norm(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws,
                           i + 1 < c.t_layers ? TL(x, i + 1, "input_layernorm.weight") : nullptr, eps, x->dHn);
             continue;

@@ -66,6 +66,10 @@ struct GemvArgs {
     float normalizer;
     int64_t pad_id;
     uint16_t* emb_out;
+    // batched decode (MFMA forms, B >= 3): the post-attention RMSNorm's sum of squares, carried from
+    // o_proj to gate|up instead of a k_rows_norm pass.  GV_RES (one K slice) writes each row's partial
+    // over its 16-column unit group, [nb][K / 16]; GV_GEGLU (unstaged) reads them, x being the raw h
+    float* ssq;
 };
 
 // WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their

@@ -96,11 +96,12 @@ void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_
 }
 
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
-                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out) {
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq) {
     GemvArgs a{};
     a.x = nullptr; a.norm_w = nullptr; a.W = Wo; a.n_units = N; a.K = G * 256; a.nb = B; a.out = h_inout;
     a.part = part; a.max_chunks = max_chunks; a.G = G; a.st = st; a.o_out = o_out;
     if (B >= gemv_mf_min_batch() && o_out) {
+        a.ssq = ssq;
         gemv_mf_ores(s, a, o_out);
         return;
     }
@@ -113,10 +114,11 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
 }
 
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* Wgu,
-                int I, uint16_t* act) {
+                int I, uint16_t* act, float* ssq) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
     if (B >= gemv_mf_min_batch()) {
+        a.ssq = norm_w ? ssq : nullptr;
         gemv_mf_geglu(s, a);
         return;
     }

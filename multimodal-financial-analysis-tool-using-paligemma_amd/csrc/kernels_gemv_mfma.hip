@@ -101,8 +101,9 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
 // group multiplies -- two register buffers in ping-pong, every issue unconditional (groups past the
 // end read one 64-B line of the matrix: all lanes the same address, results discarded), so the
 // compiler's in-order vmcnt keeps the second stream in flight across the first's wait.
-// NS (no staging): the q|k|v / gate|up input is already RMSNorm'd (k_rows_norm / k_mf_combine_norm
-// wrote it), so each wave reads its K slice straight from global like the residual projections
+// NS (no staging): the q|k|v / gate|up input is already RMSNorm'd (k_rows_norm wrote it), so each wave
+// reads its K slice straight from global like the residual projections; or (gate|up, a.ssq) the input is
+// h and each wave normalises its slice on load from o_proj's partial sums of squares
 // Weight-stream cache policy of the register-streamed MFMA GEMVs.  Each load instruction reads 64-B
 // halves of 128-B lines (16 rows x 4 lanes of 16 B), the other half following one instruction later:
 // with the default policy the line is kept in L2 for it.  Same-box A/B (B = 8 step, tools/ab_variants.sh
@@ -214,7 +215,34 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
         return;
     }
     int grp = blockIdx.x;
-    if (grp < n_groups) issue(grp);
+    // Normalise-on-load (FOLD: gate|up, a.ssq; K = 2048): x = h, RMSNorm'd by each wave for its own K slice
+    // from the 16-column partial sums of squares o_proj's epilogue wrote (a.ssq, [nb][K / 16]).  Its
+    // loads -- the norm weight (to LDS, nws, not 64 registers per lane beside the weight stream), the raw
+    // h slice, the row's partials -- are issued BEFORE the weight stream, so the in-order vmcnt of their
+    // waits leaves the stream in flight while the norm is computed.  Rows n >= nb re-read row nb - 1: they
+    // only feed C rows b >= nb, which are never stored.
+    constexpr bool FOLD = NS && MODE == GV_GEGLU;
+    constexpr int KF = 2048, Q4 = KF / 64;
+    __shared__ __attribute__((aligned(16))) uint16_t nws[FOLD ? KF : 8];
+    const bool fold = FOLD && a.ssq;
+    short8 xf[NKB][4];
+    uint4 nw0 = make_uint4(0, 0, 0, 0);
+    f32x4 sv[FOLD ? Q4 / 4 : 1];
+    if (fold) {
+        const int row = n < a.nb ? n : a.nb - 1;
+        if (tid * 8 < KF) nw0 = ldg16(a.norm_w + tid * 8);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xf[kb][i] = __builtin_bit_cast(short8, ldg16(a.x + (long)row * KF + k0 + kb * 128 + 32 * i + 8 * g));
+        const f32x4* sp = reinterpret_cast<const f32x4*>(a.ssq + (long)row * (KF / 16) + g * Q4);
+#pragma unroll
+        for (int c = 0; c < (FOLD ? Q4 / 4 : 1); ++c) sv[c] = sp[c];
+    }
+    // unconditional (a workgroup past the last group streams that group again, unused): no branch around
+    // the stream, so the waits for the loads above are counted past it
+    issue(grp < n_groups ? grp : n_groups - 1);
     // RoPE operands of this workgroup's first group, fetched with the weight stream (the epilogue
     // would otherwise pay their round trip after the reduction)
     float cs0 = 0.f, sn0 = 0.f;
@@ -228,7 +256,6 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     const int grp0 = grp;
 
     // ---- activations: this wave's K slice, MFMA A layout (row b = lane & 15)
-    short8 xf[NKB][4];
     if constexpr (STAGE) {
         mf_stage_rows(a, K, mfs, ld, red);
         __syncthreads();
@@ -238,6 +265,28 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
             for (int i = 0; i < 4; ++i)
                 xf[kb][i] = n < a.nb ? *reinterpret_cast<const short8*>(mfs + n * ld + k0 + kb * 128 + 32 * i + 8 * g)
                                      : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else if (fold) {
+        // the row's rstd: lane group g sums its quarter of the partials in order, the quarters meet over two
+        // lane swaps (the same tree in every lane of the row); then bf16((h * r) * (1 + w)) as k_rows_norm
+        if (tid * 8 < KF) *reinterpret_cast<uint4*>(nws + tid * 8) = nw0;
+        __syncthreads();
+        float ss = 0.f;
+#pragma unroll
+        for (int c = 0; c < (FOLD ? Q4 / 4 : 1); ++c) { ss += sv[c][0]; ss += sv[c][1]; ss += sv[c][2]; ss += sv[c][3]; }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        const float r = 1.0f / sqrtf(ss / (float)KF + a.eps);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u16x8 wv = *reinterpret_cast<const u16x8*>(nws + k0 + kb * 128 + 32 * i + 8 * g);
+                const u16x8 e = __builtin_bit_cast(u16x8, xf[kb][i]);
+                u16x8 o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e.v[j]) * r) * (1.0f + bf2f(wv.v[j])));
+                xf[kb][i] = __builtin_bit_cast(short8, o);
+            }
     } else {
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
@@ -313,6 +362,33 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 }
             }
             continue;
+        }
+        if constexpr (MODE == GV_RES) {
+            if (KS == 1) {
+                // h += o_proj(x); with a.ssq, each row's sum of squares of the new h over this group's 16
+                // columns (the next RMSNorm's partial, read by gate|up): a fixed butterfly over lanes n
+                float q[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int b = 4 * g + r;
+                    q[r] = 0.f;
+                    if (b < a.nb && u < a.n_units) {
+                        const long o = (long)b * a.n_units + u;
+                        const uint16_t v = f2bf(rbf(acc[0][r]) + bf2f(a.out[o]));
+                        a.out[o] = v;
+                        q[r] = bf2f(v) * bf2f(v);
+                    }
+                }
+                if (a.ssq) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                        for (int o = 1; o < 16; o <<= 1) q[r] += __shfl_xor(q[r], o, 64);
+                        if (n == 0 && 4 * g + r < a.nb) a.ssq[(long)(4 * g + r) * n_groups + cur] = q[r];
+                    }
+                }
+                continue;
+            }
         }
         if (u >= a.n_units) continue;
 #pragma unroll
@@ -750,7 +826,8 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
     // (k_gemv_ml, 4 waves x 3-deep rings); 256 / 384 / 1,024 workgroups and 2 or 8 K-split waves
     // measured slower (1.746-2.051 ms); the unstaged form re-swept in round 4 (profiles/r04_gu_blocks_ab.txt:
     // 512 best against 384 / 768 / 1,024)
-    if (a.norm_w) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
+    // (a.ssq: x = h, normalised on load from o_proj's partial sums of squares -- unstaged, norm_w read)
+    if (a.norm_w && !a.ssq) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
     else launch_mf<GV_GEGLU, 2, 512, 4, 1, true>(s, a, 512, 1, nullptr);  // input already normed
 }
 

@@ -95,12 +95,15 @@ void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_
 // hn[b] = RMSNorm(x[b]) for nb rows of K (one workgroup per row)
 void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, int nb, int K, uint16_t* out);
 // o_proj + residual whose input is the combine of the decode-attention partials (MQA:
-// n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output
+// n_kv = 1, G heads of 256); o_out (optional) receives the combined bf16 attention output.
+// ssq (batched MFMA form only, else ignored): each row's 16-column partial sums of squares of the
+// new h, [B][N / 16] -- the next RMSNorm's, read by gemv_geglu
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
-                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out);
-
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq = nullptr);
+// fused RMSNorm + gate|up + GeGLU; ssq (B >= gemv_mf_min_batch() only): h's RMSNorm from the
+// partials gemv_o_attn wrote instead of the row pass
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
-                const uint16_t* Wgu, int I, uint16_t* act);
+                const uint16_t* Wgu, int I, uint16_t* act, float* ssq = nullptr);
 int gemv_logits_blocks();
 int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 // done/next/adv (decode, may be null): fold the argmax into the launch's last workgroup and

@@ -18,8 +18,10 @@ the cache's length and is overwritten.  After two misses in a row the lookahead 
 cache (a sampling loop, inference.py:64-66, would otherwise pay a wasted step per token).
 
 Ordering: the lookahead uses the engine's workspace and the cache's slab, so (1) the side stream waits for
-the caller's stream before every lookahead, (2) every later engine call on any other stream waits for the
-last lookahead (Engine._s() runs the guard installed here), and (3) the slab is marked as used by the side
+the caller's stream before a lookahead that follows a step (or any engine call) on the caller's stream --
+after a hit it follows its own previous step and waits for nothing else, so the caller's check and per-token
+ops stay off the chain of steps, (2) every later engine call on any other stream waits for the last
+lookahead (Engine._s() runs the guard installed here), and (3) the slab is marked as used by the side
 stream for the caching allocator.  Three ids / logits slots rotate, so the token check of one step never
 races the write of the step after it.  What the caller gets is bit-identical to the step run on demand:
 the same graphed step over the same inputs.
@@ -48,26 +50,36 @@ class GreedyLookahead:
         self.pending = None    # (weakref to the KVCache, kv_len, position, slot, event on the side stream)
         self.last = None       # event of the last lookahead enqueued (what other streams must wait for)
         self.hits = 0
+        self.main_touched = False  # an engine call ran on another stream since the last lookahead
         eng._stream_guard = self._guard
 
     def _guard(self, handle) -> None:
-        """Engine._s(): an engine call about to run on stream `handle` waits for the last lookahead."""
-        if self.last is not None and handle != self.side.cuda_stream:
-            torch.cuda.current_stream(self.eng.device).wait_event(self.last)
+        """Engine._s(): an engine call about to run on stream `handle` waits for the last lookahead (and the
+        next lookahead will wait for it: it shares the engine's workspace)."""
+        if handle != self.side.cuda_stream:
+            self.main_touched = True
+            if self.last is not None:
+                torch.cuda.current_stream(self.eng.device).wait_event(self.last)
 
     def _run(self, slab, kv_len, position, s, graph):
         self.eng.decode(self.ids[s], slab, kv_len, position, logits=self.logits[s],
                         next_ids=self.ids[(s + 1) % NSLOT], graph=graph)
 
-    def _ahead(self, kv_cache, slab, kv_len, position, s, graph):
-        """Enqueue on the side stream the step in slot s (its input ids[s]: the previous step's argmax)."""
+    def _ahead(self, kv_cache, slab, kv_len, position, s, graph, after_main: bool):
+        """Enqueue on the side stream the step in slot s (its input ids[s]: the previous step's argmax).
+        after_main: the previous step ran on the caller's stream, so the side stream waits for it; after a
+        hit (and no engine call on another stream since the last lookahead) the previous step is the side
+        stream's own last one and nothing on the caller's stream is waited for -- the caller's check, clone
+        and own ops stay off the chain of steps (slots read on the caller's stream are rewritten three steps
+        later, behind the host's wait for that step's check)."""
         if kv_len + 1 > slab.shape[3] or getattr(kv_cache, "_pgmi_misses", 0) >= 2:
             self.pending = None
             return
-        main = torch.cuda.current_stream(self.eng.device)
-        ready = torch.cuda.Event()
-        ready.record(main)
-        self.side.wait_event(ready)
+        if after_main or self.main_touched:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.eng.device))
+            self.side.wait_event(ready)
+        self.main_touched = False
         with torch.cuda.stream(self.side):
             self._run(slab, kv_len, position, s, graph)
             ev = torch.cuda.Event()
@@ -95,7 +107,7 @@ class GreedyLookahead:
             if after_launch is not None:
                 after_launch()
             # the next lookahead goes in before the host waits for the check: the GPU keeps running
-            self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph)
+            self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph, False)
             self.ev_chk.synchronize()
             if not bool(self.flag):
                 kv_cache._pgmi_misses = 0
@@ -115,7 +127,7 @@ class GreedyLookahead:
         out = self.logits[s].clone().unsqueeze(1)
         if after_launch is not None:
             after_launch()
-        self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph)
+        self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph, True)
         return out
 
 

@@ -33,6 +33,8 @@ def logit_stats(label, ours, ref_bf16, ref_fp32=None):
         st.update({"ref_bf16_vs_fp32_mean": float(floor.mean()), "ref_bf16_vs_fp32_max": float(floor.max()),
                    "ours_vs_fp32_mean": float(ofp.mean()), "ours_vs_fp32_max": float(ofp.max()),
                    "per_step_ratio_max": float((per / np.maximum(floor, 1e-30)).max())})
+        over = per > REL_L2_RULE  # the steps the floor rule governs (the rest pass on the 2e-2 bound)
+        st["floor_ratio_max_over_2e-2"] = float((per[over] / np.maximum(floor[over], 1e-30)).max()) if over.any() else 0.0
         st["_per"], st["_floor"] = per, floor
     print("parity " + json.dumps({k: v for k, v in st.items() if not k.startswith("_")}))
     path = os.environ.get("PGMI_PARITY_LOG")
@@ -42,8 +44,11 @@ def logit_stats(label, ours, ref_bf16, ref_fp32=None):
     return st
 
 
-STEP_FLOOR_FACTOR = 1.6   # per step: rel-L2 vs reference bf16 <= max(2e-2, 1.6 x the reference's own error)
+STEP_FLOOR_FACTOR = 1.45  # per step: rel-L2 vs reference bf16 <= max(2e-2, 1.45 x the reference's own error)
 MEAN_FLOOR_FACTOR = 1.25  # over the steps: mean <= max(2e-2, 1.25 x the reference's mean error)
+# module-level chains (assert_within_floor: one layer or block against the oracle, base 1e-2) keep the
+# round-4 factor: their floors are a single module's rounding noise, not a whole model's
+MODULE_FLOOR_FACTOR = 1.6
 
 
 def assert_step_rule(st, step_factor=STEP_FLOOR_FACTOR, mean_factor=MEAN_FLOOR_FACTOR):
@@ -146,7 +151,7 @@ def remove_ablation_patches(model):
         layer.self_attn.rotary_emb.__dict__.pop("forward", None)
 
 
-def assert_within_floor(label, got, ref_bf16, ref_fp32, base=1e-2, factor=STEP_FLOOR_FACTOR):
+def assert_within_floor(label, got, ref_bf16, ref_fp32, base=1e-2, factor=MODULE_FLOOR_FACTOR):
     """Module-level form of the floor rule: rel-L2 of our output vs the oracle bf16
     <= max(base, factor x the oracle bf16's own rel-L2 vs its fp32 truth) -- for module chains whose
     bf16 rounding noise alone approaches the kernel-level 1e-2 bound (a Gemma attention: 0.96e-2, a

@@ -587,8 +587,9 @@ class PaliGemmaForConditionalGeneration(nn.Module):
 
         if self._merge_is_patched() or inputs_embeds is not None:
             # generic path: the (patched) merge decides embeddings / positions
+            own_embeds = None
             if inputs_embeds is None:
-                inputs_embeds = eng.embed(input_ids)
+                inputs_embeds = own_embeds = eng.embed(input_ids)
             if pixel_values is not None:
                 img = eng.project(eng.vision(pixel_values))
             else:
@@ -602,9 +603,16 @@ class PaliGemmaForConditionalGeneration(nn.Module):
                 # ablation_study_fixed.py:215-221,239-243): the graphed decode step reads the merge's
                 # position and additive mask on the device -- no host read before the step is enqueued
                 slab = kv_cache._ensure(eng, B, cache_len + 1)
-                logits = eng.decode_embeds_dev(merged[:, 0], slab, cache_len, position_ids,
-                                               mask if torch.is_tensor(mask) else None, logits=eng.logits_buffer(B),
-                                               graph=self.pgmi_use_graph).clone().unsqueeze(1)
+                if self.pgmi_lookahead and self.pgmi_use_graph and own_embeds is not None:
+                    # the greedy continuation one step ahead of the harness (pgmi/lookahead.py): used when the
+                    # merge passed this token's embedding through at the predicted position with a zero mask
+                    logits = lookahead_for(eng, B).step_embeds(kv_cache, slab, input_ids, own_embeds, merged[:, 0],
+                                                               position_ids, mask if torch.is_tensor(mask) else None,
+                                                               cache_len, True)
+                else:
+                    logits = eng.decode_embeds_dev(merged[:, 0], slab, cache_len, position_ids,
+                                                   mask if torch.is_tensor(mask) else None, logits=eng.logits_buffer(B),
+                                                   graph=self.pgmi_use_graph).clone().unsqueeze(1)
                 chk.wait()
                 kv_cache._len = cache_len + 1
                 return self._pack(logits, labels, kv_cache, return_dict)

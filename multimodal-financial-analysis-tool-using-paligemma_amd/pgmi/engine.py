@@ -232,7 +232,9 @@ class Engine:
         self._ready()
         i = ids.to(self.device, torch.int64).contiguous()
         out = torch.empty(tuple(i.shape) + (self.cfgd["t_hidden"],), dtype=torch.bfloat16, device=self.device)
-        N.check(self.lib.pgmi_embed(self.ctx, i.data_ptr(), i.numel(), out.data_ptr(), self._s()), "pgmi_embed")
+        # (a plain lookup into a fresh tensor: no engine workspace, so no wait for a lookahead in flight)
+        N.check(self.lib.pgmi_embed(self.ctx, i.data_ptr(), i.numel(), out.data_ptr(), N.stream_handle(self.device)),
+                "pgmi_embed")
         return out
 
     def lm_forward(self, kv: torch.Tensor, kv_start: int, positions, ids=None, image_feats=None, embeds=None,
@@ -311,7 +313,8 @@ class Engine:
     _POS_DTYPES = {torch.bfloat16: 0, torch.float32: 2, torch.int64: 10, torch.int32: 11, torch.float64: 12}
 
     def decode_embeds_dev(self, embeds: torch.Tensor, kv: torch.Tensor, kv_len: int, position: torch.Tensor,
-                          mask: torch.Tensor = None, logits: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
+                          mask: torch.Tensor = None, logits: torch.Tensor = None, graph: bool = False,
+                          next_ids: torch.Tensor = None) -> torch.Tensor:
         """decode_embeds for one sequence with its rotary position and additive mask left on the device
         (a merge's outputs, read by the step itself: no host sync).  position: one element; mask:
         kv_len + 1 additive values (bf16 or fp32; other float dtypes are promoted to fp32)."""
@@ -336,8 +339,8 @@ class Engine:
             logits = torch.empty((1, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
         N.check(self.lib.pgmi_decode_embeds_dev(self.ctx, e.data_ptr(), 1, kv.data_ptr(), kv.shape[2], kv.shape[3],
                                                 kv_len, p.data_ptr(), self._POS_DTYPES[p.dtype], N.ptr(mp), mdt,
-                                                mp.numel() if mp is not None else 0, logits.data_ptr(), None,
-                                                int(graph), self._s()),
+                                                mp.numel() if mp is not None else 0, logits.data_ptr(),
+                                                N.ptr(next_ids), int(graph), self._s()),
                 "pgmi_decode_embeds_dev")
         return logits
 

@@ -10,11 +10,13 @@ asked for, it enqueues the step whose input is that step's on-device argmax (tor
 written by the lm_head's last workgroup) into another logits buffer and the next KV row.  The caller's own
 ops (its argmax, `.item()`) stay on its stream and do not wait for it, so the GPU runs the next step while
 the host does its per-token work.  When the caller's next forward() brings that same token at the next
-position of the same cache, its stream waits for the lookahead (a GPU-side event), checks the token
-against the one the lookahead used, hands back the lookahead's logits and enqueues the following
-lookahead; the host waits only for the check.  Any other input (a sampled token, another position,
-another cache) runs the asked step on the caller's stream behind the lookahead, whose KV row lies past
-the cache's length and is overwritten.  After two misses in a row the lookahead stands down for that
+position of the same cache, its stream checks the token against the one the lookahead used, the following
+lookahead is enqueued, the host waits for the check and the lookahead, and the caller's stream copies the
+lookahead's logits out -- the caller's stream never waits on the side stream (a pending cross-queue wait
+slows the other queue's graphed step by ~0.09 ms: tools/probes/stream_probe.py, profiles/
+r05_stream_probe.txt), and nothing runs between two lookaheads on the side stream.
+Any other input (a sampled token, another position, another cache) runs the asked step on the caller's
+stream behind the lookahead, whose KV row lies past the cache's length and is overwritten.  After two misses in a row the lookahead stands down for that
 cache (a sampling loop, inference.py:64-66, would otherwise pay a wasted step per token).
 
 Ordering: the lookahead uses the engine's workspace and the cache's slab, so (1) the side stream waits for
@@ -88,6 +90,32 @@ class GreedyLookahead:
         self.last = ev
         self.pending = (weakref.ref(kv_cache), kv_len, position, s, ev)
 
+    def _take(self, kv_cache, slab, cache_len, position, s, done, ne, graph, after_launch):
+        """The hit path's tail: ne (a device bool, on the caller's stream) says whether the asked step differs
+        from the lookahead in slot s (done: its event on the side stream).  Hands back the lookahead's logits
+        (None on a miss)."""
+        main = torch.cuda.current_stream(self.eng.device)
+        self.flag.copy_(ne, non_blocking=True)
+        self.ev_chk.record(main)
+        if after_launch is not None:
+            after_launch()
+        # the next lookahead goes in before the host waits: the side stream never runs dry
+        self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph, False)
+        # the host waits for the check and for the lookahead itself; the caller's stream then copies its
+        # logits out with no GPU-side wait on the side stream (a pending cross-queue wait slows the other
+        # queue's steps by ~9 %: tools/probes/stream_probe.py), and nothing sits between two lookaheads
+        self.ev_chk.synchronize()
+        done.synchronize()
+        if not bool(self.flag):
+            kv_cache._pgmi_misses = 0
+            self.hits += 1
+            return self.logits[s].clone().unsqueeze(1)
+        # a miss (sampling, a forced token): the asked step runs on the caller's stream behind the
+        # lookahead just enqueued, over the same KV rows
+        kv_cache._pgmi_misses = getattr(kv_cache, "_pgmi_misses", 0) + 1
+        self.pending = None
+        return None
+
     def step(self, kv_cache, slab, input_ids, cache_len: int, position: int, graph: bool, after_launch=None):
         """The logits (B, 1, V) of the decode step for input_ids at KV row cache_len / rotary `position`
         (a fresh tensor, as the reference returns); `after_launch` runs once the asked step is enqueued."""
@@ -99,24 +127,12 @@ class GreedyLookahead:
         if (p is not None and p[0]() is kv_cache and p[1] == cache_len and p[2] == position
                 and ids.numel() == self.B):
             s = p[3]
-            main.wait_event(p[4])  # the lookahead in slot s has run: its logits and its input token are final
-            ne = torch.ne(ids, self.ids[s]).any()
-            self.flag.copy_(ne, non_blocking=True)
-            self.ev_chk.record(main)
-            out = self.logits[s].clone().unsqueeze(1)
-            if after_launch is not None:
-                after_launch()
-            # the next lookahead goes in before the host waits for the check: the GPU keeps running
-            self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph, False)
-            self.ev_chk.synchronize()
-            if not bool(self.flag):
-                kv_cache._pgmi_misses = 0
-                self.hits += 1
+            # the check on the caller's stream: the lookahead's input ids[s] was written by the step before
+            # it, which the host has already waited for, so nothing here waits for the side stream
+            out = self._take(kv_cache, slab, cache_len, position, s, p[4], torch.ne(ids, self.ids[s]).any(), graph,
+                             after_launch)
+            if out is not None:
                 return out
-            # a miss (sampling, a forced token): the asked step runs on the caller's stream behind the
-            # lookahead just enqueued (Engine._s() makes it wait), over the same KV rows
-            kv_cache._pgmi_misses = getattr(kv_cache, "_pgmi_misses", 0) + 1
-            self.pending = None
             s = (s + 2) % NSLOT
         # the asked step on the caller's stream, behind any lookahead still in flight (it shares the slots,
         # the engine's workspace and possibly this cache's rows)
@@ -128,6 +144,41 @@ class GreedyLookahead:
         if after_launch is not None:
             after_launch()
         self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % NSLOT, graph, True)
+        return out
+
+    def step_embeds(self, kv_cache, slab, input_ids, embeds, row, position, mask, cache_len: int, graph: bool):
+        """The ablation harness's q_len == 1 step (ablation_study_fixed.py:215-221,239-243: its patched merge,
+        then pgmi_decode_embeds_dev over the merged row, the merge's device position and additive mask).
+        embeds: this call's own lookup of input_ids (Engine.embed); row: the merge's output row.  The
+        lookahead (the ids step at the predicted next position, no mask) stands for the asked step when the
+        token is the lookahead's, the merge passed its embedding through unchanged, the position is the
+        predicted one and the mask is all zeros -- the same arithmetic (a zero additive mask leaves every
+        bf16 score as it is), checked on the device.  Otherwise the asked step runs on the caller's stream."""
+        main = torch.cuda.current_stream(self.eng.device)
+        ids = input_ids.reshape(-1).to(self.eng.device, torch.int64)
+        p = self.pending
+        self.pending = None
+        s = 0
+        if p is not None and p[0]() is kv_cache and p[1] == cache_len and ids.numel() == 1 == self.B:
+            s = p[3]
+            ne = torch.ne(ids, self.ids[s]).any()
+            ne = ne | torch.ne(row.reshape(-1), embeds.reshape(-1)).any()
+            ne = ne | torch.ne(torch.round(position.reshape(-1)[:1].to(torch.float64)), float(p[2])).any()
+            if mask is not None:
+                ne = ne | torch.ne(mask, 0).any()
+            out = self._take(kv_cache, slab, cache_len, p[2], s, p[4], ne, graph, None)
+            if out is not None:
+                return out
+            s = (s + 2) % NSLOT
+        # the asked step on the caller's stream; the next lookahead's position is the merge's position + 1,
+        # read on the host before the step is enqueued (the read waits for the merge's own ops only)
+        pos = int(round(float(position.reshape(-1)[0].item())))
+        if self.last is not None:
+            main.wait_event(self.last)
+        lg = self.eng.decode_embeds_dev(row, slab, cache_len, position, mask, logits=self.logits[s],
+                                        next_ids=self.ids[(s + 1) % NSLOT], graph=graph)
+        out = lg.clone().unsqueeze(1)
+        self._ahead(kv_cache, slab, cache_len + 1, pos + 1, (s + 1) % NSLOT, graph, True)
         return out
 
 

@@ -118,6 +118,9 @@ def test_ablation_kv_mode_teacher_forced(model, G):
         calls.append(1)
         return orig(*a, **k)
 
+    from pgmi.lookahead import lookahead_for
+    la = lookahead_for(eng, 1)
+    hits0 = la.hits
     eng.decode_embeds_dev = counting
     try:
         n = len(g["kv_tokens"])
@@ -125,8 +128,10 @@ def test_ablation_kv_mode_teacher_forced(model, G):
     finally:
         del eng.decode_embeds_dev
     # every q_len == 1 step took the graphed decode step over the merged row, with the merge's position
-    # and mask read on the device (pgmi_decode_embeds_dev: no host read per step)
-    assert len(calls) == n - 1
+    # and mask read on the device (pgmi_decode_embeds_dev: no host read per step), or the greedy lookahead
+    # that stands for it (pgmi/lookahead.py step_embeds: the same step, checked on the device)
+    assert len(calls) + (la.hits - hits0) == n - 1
+    assert la.hits - hits0 > (n - 1) // 2
     top = torch.gather(pre[0], 0, torch.from_numpy(g["kv_prefill_topk_idx"][0]).cuda()).cpu().numpy()
     assert np.abs(top - g["kv_prefill_topk_val"][0]).max() <= 0.25
     _check(logits, picks, g, "kv", G["ab_fp32"])
@@ -173,4 +178,46 @@ def test_patched_merge_nonzero_mask_is_refused(model, G):
         with pytest.raises(NotImplementedError):
             model(input_ids=ids, pixel_values=px, attention_mask=torch.ones_like(ids), kv_cache=MG.KVCache())
     finally:
+        model._merge_input_ids_with_image_features = base
+
+
+@torch.no_grad()
+def test_ablation_lookahead_bit_identical(model, G):
+    """The harness's q_len == 1 steps through the greedy lookahead (pgmi/lookahead.py step_embeds) return
+    exactly what pgmi_decode_embeds_dev returns on demand: 24 KV-mode tokens with the lookahead on and off,
+    every step's logits and pick bit for bit, free-running and teacher-forced on the reference's tokens
+    (where they differ from ours: misses), and a merge that changes the row is never taken for a hit."""
+    import types
+    from pgmi.lookahead import lookahead_for
+    g = G["ab"]
+    ids = torch.from_numpy(g["ids"]).cuda()
+    px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    la = lookahead_for(model._pgmi_engine(), 1)
+    for teacher in (None, g["kv_tokens"][:24]):
+        res = []
+        for on in (True, False):
+            model.pgmi_lookahead = on
+            try:
+                res.append(run_harness(model, ids, px, True, 24, teacher=teacher))
+            finally:
+                model.pgmi_lookahead = True
+        assert torch.equal(res[0][0], res[1][0])
+        assert np.array_equal(res[0][1], res[1][1])
+    # a merge that scales the text rows: every step must run on demand (no hit), and match the on-demand run
+    base = model._merge_input_ids_with_image_features
+
+    def scaled(self, *a, **k):
+        e, m, p = base(*a, **k)
+        return e * 2, m, p
+
+    model._merge_input_ids_with_image_features = types.MethodType(scaled, model)
+    try:
+        hits0 = la.hits
+        on = run_harness(model, ids, px, True, 6)[0]
+        assert la.hits == hits0
+        model.pgmi_lookahead = False
+        off = run_harness(model, ids, px, True, 6)[0]
+        assert torch.equal(on, off)
+    finally:
+        model.pgmi_lookahead = True
         model._merge_input_ids_with_image_features = base

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: the lookahead on a hipStreamNonBlocking side stream -- drop-in tests, the loop's timeline, the bench's
+# drop-in numbers; batch tests for k_mf_combine_norm keeping its row in registers.
+set -e
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r5k
+mkdir -p $OUT
+T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+timeout -k 10 300 $T $R/tests/test_gpu_full_api.py $R/tests/test_gpu_full_batch.py > $OUT/tests.log 2>&1
+timeout -k 10 300 python3 -u $R/tools/probes/lookahead_probe.py > $OUT/lookahead_probe.txt 2>&1
+timeout -k 10 300 python3 -u $R/bench.py --no-448 --no-cpu-baseline --prefill-iters 3 --steps 64 --nokv-tokens 2 \
+    > $OUT/bench.json 2> $OUT/bench.err
+echo done

@@ -45,7 +45,7 @@ def main():
             assert hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(flags), ctypes.c_int(prio)) == 0
         return torch.cuda.ExternalStream(h.value)
 
-    def run(label, side, rotate, extra, graph=True):
+    def run(label, side, rotate, extra, graph=True, waits=False, nowait=False):
         kv = e.new_kv(1, 576)
         feats = e.project(e.vision(px))
         e.lm_forward(kv, 0, torch.arange(L)[None], ids=ids0, image_feats=feats, logits_rows=1)
@@ -64,13 +64,16 @@ def main():
                 a.record()
                 e.decode(ids[s], kv, L + t, L + t + 1, logits=lg[s], next_ids=nxt, graph=graph)
                 b.record()
+            if waits and t > 0:
+                main.wait_event(prev)  # the caller's stream waits for the previous step (a barrier packet)
             if extra:
                 _ = torch.ne(ids[s], ids[(s + 2) % 3]).any()
                 _ = lg[(s + 2) % 3].clone()
                 _ = torch.argmax(lg[(s + 2) % 3], dim=-1)
+            prev = b
             if t >= 8:
                 evs.append((a, b))
-            if side and t % 4 == 3:
+            if side and t % 4 == 3 and not nowait:
                 main.wait_stream(st)
         torch.cuda.synchronize()
         du = [a.elapsed_time(b) * 1e3 for a, b in evs]
@@ -79,11 +82,19 @@ def main():
               f"wall per step {span:.1f} us")
 
     print("current stream", torch.cuda.current_stream(), "null?", torch.cuda.current_stream().cuda_stream)
+    nb = hip_stream(1)
     for _ in range(2):
+        run("A main, fixed buffers", False, False, False)
+        run("Hf non-blocking side, fixed buffers", nb, False, False)
+        run("Hn non-blocking side, the caller's stream never waits for it", nb, False, False, nowait=True)
+        run("Hs torch side stream, the caller's stream never waits for it", True, False, False, nowait=True)
+        run("H2n non-blocking side, caller's small ops, no waits", nb, True, True, nowait=True)
+    for _ in range(0):
         run("A main, fixed buffers", False, False, False)
         run("B side, fixed buffers", True, False, False)
         run("C main, rotating slots", False, True, False)
         run("D side, rotating slots + caller ops", True, True, True)
+    return
     run("E main, eager (no graph)", False, False, False, graph=False)
     run("F side, eager (no graph)", True, False, False, graph=False)
     run("G torch stream priority -1", torch.cuda.Stream(priority=-1), False, False)

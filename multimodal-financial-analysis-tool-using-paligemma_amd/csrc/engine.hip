@@ -103,6 +103,9 @@ struct pgmi_ctx {
     uint16_t *dH, *dQ, *dAO, *dACT;
     uint16_t* dHn;  // batched decode (B >= 3): the RMSNorm'd rows the unstaged MFMA projections read
     float* dSS;     // batched decode: o_proj's 16-column partial sums of squares of h, [B][H / 16]
+    // batched decode (max_batch >= 3): the fragment-major image of every layer's gate|up weights (mf_swizzle),
+    // [layer][2 I x H]
+    uint16_t* mfw = nullptr;
     float *opart, *pmax, *dlogits, *amax_v;
     int *pidx, *amax_i;
     int max_chunks;
@@ -628,6 +631,13 @@ int pgmi_prepare(pgmi_ctx* x) {
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
     LAUNCHCHK();
+    if (c.max_batch >= gemv_mf_min_batch() && c.t_intermediate % 32 == 0 && c.t_hidden % 32 == 0) {
+        const size_t I = c.t_intermediate, H = c.t_hidden, per = 2 * I * H;
+        if (!x->mfw && (rc = dalloc_t(x, &x->mfw, per * c.t_layers))) return rc;
+        for (int i = 0; i < c.t_layers; ++i)  // gate rows, then up rows (adjacent slots)
+            mf_swizzle(nullptr, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, x->mfw + per * i);
+        LAUNCHCHK();
+    }
     std::vector<uint16_t> cs, sn;
     if (!x->host_cos.empty()) {
         cs = x->host_cos;
@@ -987,8 +997,10 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         if (mf) {
             // the post-attention RMSNorm: its sums of squares come from o_proj's epilogue (dSS), gate|up
             // normalises h on load (no k_rows_norm pass: B = 8 step -5 us per layer)
+            // gate|up from its fragment-major image (prepare's mf_swizzle), when built
+            const uint16_t* Lf = x->mfw ? x->mfw + (size_t)2 * c.t_intermediate * H * i : nullptr;
             gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
-                       c.t_intermediate, x->dACT, x->dSS);
+                       c.t_intermediate, x->dACT, x->dSS, Lf);
             gemv_res_norm(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws,
                           i + 1 < c.t_layers ? TL(x, i + 1, "input_layernorm.weight") : nullptr, eps, x->dHn);
             continue;

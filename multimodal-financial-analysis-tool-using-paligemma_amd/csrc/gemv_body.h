@@ -70,6 +70,9 @@ struct GemvArgs {
     // o_proj to gate|up instead of a k_rows_norm pass.  GV_RES (one K slice) writes each row's partial
     // over its 16-column unit group, [nb][K / 16]; GV_GEGLU (unstaged) reads them, x being the raw h
     float* ssq;
+    // batched decode (MFMA forms): the weight matrix's fragment-major image (k_mf_swizzle, built at prepare),
+    // read instead of W when set (gate|up: the gate rows' image, then the up rows')
+    const uint16_t* Wf;
 };
 
 // WK waves split one unit group's K range (WK = 4 for the 16384-wide down_proj), their

@@ -114,11 +114,12 @@ void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks,
 }
 
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* Wgu,
-                int I, uint16_t* act, float* ssq) {
+                int I, uint16_t* act, float* ssq, const uint16_t* Wf) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wgu; a.n_units = I; a.K = 2048; a.nb = B; a.I = I; a.out = act;
     if (B >= gemv_mf_min_batch()) {
         a.ssq = norm_w ? ssq : nullptr;
+        a.Wf = I % 16 == 0 ? Wf : nullptr;
         gemv_mf_geglu(s, a);
         return;
     }

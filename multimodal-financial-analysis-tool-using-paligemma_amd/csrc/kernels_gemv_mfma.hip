@@ -94,6 +94,26 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
     else mf_stage_rows_t<MF_MAXB>(a, K, xs, ld, red, k0, ksl);
 }
 
+// Fragment-major weight image for the batched (MFMA) decode GEMVs, built once at prepare: the 16-row x 32-k
+// block (g, kb) of a [rows][K] matrix is stored as the 64 lanes' B fragments in lane order -- lane
+// (n = l & 15, g = l >> 4) holds row 16 g_row + n, k = 32 kb + 8 g .. + 8 -- so one load instruction of a
+// wave reads 1 KiB contiguous (the row-major image: 16 rows x 64 B, half lines whose other halves come one
+// instruction later).  Element offset of (row group gr, k block kb, lane l) = ((gr * K / 32 + kb) * 64 + l) * 8.
+__global__ void k_mf_swizzle(const uint16_t* __restrict__ W, int K, long n_chunks, uint16_t* __restrict__ out) {
+    const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 16-B chunk per thread
+    if (c >= n_chunks) return;
+    const int l = (int)(c & 63);
+    const long blk = c >> 6, kbs = K / 32;
+    const long gr = blk / kbs, kb = blk % kbs;
+    const long row = gr * 16 + (l & 15), k = kb * 32 + 8 * (l >> 4);
+    *reinterpret_cast<uint4*>(out + c * 8) = ldg16(W + row * K + k);
+}
+
+void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out) {
+    const long n = (long)rows * K / 8;
+    hipLaunchKernelGGL(k_mf_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, K, n, out);
+}
+
 // MODE: GV_*; NR: weight rows per unit (2: RoPE / GeGLU pairs); KW: K elements per wave; WK:
 // waves per unit group (K split inside the workgroup).  grid.x: unit-group slots (grid-stride
 // over groups), grid.y: KS (K split over workgroups; GV_RES only, partials to ws).
@@ -112,11 +132,12 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
 #ifndef PGMI_MF_NT
 #define PGMI_MF_NT 2
 #endif
-template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false>
+template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false, bool SW = false>
 __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restrict__ ws) {
     constexpr int NKB = KW / 128;          // 128-wide k blocks per wave
     constexpr bool STAGE = (MODE != GV_RES) && !NS;
-    constexpr bool kNt = PGMI_MF_NT == 1 || (PGMI_MF_NT == 0 && MODE != GV_GEGLU);
+    // (the fragment-major image, SW: every load reads whole lines once -- non-temporal)
+    constexpr bool kNt = SW || PGMI_MF_NT == 1 || (PGMI_MF_NT == 0 && MODE != GV_GEGLU);
     extern __shared__ __attribute__((aligned(16))) uint16_t mfs[];
     __shared__ float red[MF_MAXB * 16];
     __shared__ f32x4 kred[WK][NR][64];
@@ -141,17 +162,23 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
         else return (long)u;
     };
     uint4 w[NR][NKB][4];
+    // SW: the fragment-major image (k_mf_swizzle; n_units % 16 == 0, the up rows' image of n_groups groups
+    // after the gate rows'): lane-linear 1-KiB pieces, k block stride 512 elements, read non-temporal
+    static_assert(!SW || MODE == GV_GEGLU, "fragment-major image: the gate|up GEMV");
     auto issue = [&](int grp) {
         int u = grp * 16 + n;
         if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
-            const uint16_t* rp = a.W + row_of(u, j) * K + k0 + 8 * g;
+            const uint16_t* rp = SW ? a.W + (((long)j * n_groups + grp) * (K / 32) + k0 / 32) * 512 + lane * 8
+                                    : a.W + row_of(u, j) * K + k0 + 8 * g;
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    w[j][kb][i] = kNt ? ldg_nt(rp + kb * 128 + 32 * i) : ldg16(rp + kb * 128 + 32 * i);
+                for (int i = 0; i < 4; ++i) {
+                    const long o = SW ? (long)(kb * 4 + i) * 512 : kb * 128 + 32 * i;
+                    w[j][kb][i] = kNt ? ldg_nt(rp + o) : ldg16(rp + o);
+                }
         }
     };
     if constexpr (PF == 2) {
@@ -730,6 +757,8 @@ __global__ void __launch_bounds__(256) k_mf_combine_norm(const float* __restrict
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long slab = (long)gridDim.x * N;
     float ss = 0.f;
+    // N = 2048: one chunk of 8 per thread, kept in registers for the norm (no re-read of h); wider rows re-read
+    u16x8 keep{};
     for (int c = tid * 8; c < N; c += 256 * 8) {
         const long i0 = (long)b * N + c;
         f32x4 p[8][2];
@@ -752,6 +781,7 @@ __global__ void __launch_bounds__(256) k_mf_combine_norm(const float* __restrict
             ss += f * f;
         }
         *reinterpret_cast<u16x8*>(h + i0) = o;
+        keep = o;
     }
     if (!w) return;
     ss = wave_sum(ss);
@@ -759,7 +789,8 @@ __global__ void __launch_bounds__(256) k_mf_combine_norm(const float* __restrict
     __syncthreads();
     const float r = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
     for (int c = tid * 8; c < N; c += 256 * 8) {
-        const uint4 v = ldg16(h + (long)b * N + c), wv = ldg16(w + c);  // this thread's own stores
+        const uint4 wv = ldg16(w + c);
+        const uint4 v = N <= 256 * 8 ? __builtin_bit_cast(uint4, keep) : ldg16(h + (long)b * N + c);  // own stores
         const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
         const uint16_t* we = reinterpret_cast<const uint16_t*>(&wv);
         u16x8 o;
@@ -776,16 +807,16 @@ void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, i
 // smallest lock-step batch whose decode projections run on MFMA (B <= 2: the v_dot2 GEMVs of gemv_body.h)
 int gemv_mf_min_batch() { return 3; }
 
-template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false>
+template <int MODE, int NR, int KW, int WK, int PF = 1, bool NS = false, bool SW = false>
 static void launch_mf(hipStream_t s, const GemvArgs& a, int blocks, int KS, float* ws) {
     const size_t lds = (MODE == GV_RES || NS) ? 0 : (size_t)a.nb * (a.K + 8) * sizeof(uint16_t);
     static size_t attr = 0;
     if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK, PF, NS>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemv_mf<MODE, NR, KW, WK, PF, NS, SW>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK, PF, NS>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
+    hipLaunchKernelGGL((k_gemv_mf<MODE, NR, KW, WK, PF, NS, SW>), dim3(blocks, KS), dim3(64 * WK), lds, s, a, ws);
 }
 
 static int groups_of(int units) { return (units + 15) / 16; }
@@ -827,7 +858,16 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
     // measured slower (1.746-2.051 ms); the unstaged form re-swept in round 4 (profiles/r04_gu_blocks_ab.txt:
     // 512 best against 384 / 768 / 1,024)
     // (a.ssq: x = h, normalised on load from o_proj's partial sums of squares -- unstaged, norm_w read)
-    if (a.norm_w && !a.ssq) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
+    // a.Wf: the fragment-major weight image (1-KiB lane-linear loads; the decode step passes it)
+    const bool staged = a.norm_w && !a.ssq;
+    if (a.Wf) {
+        GemvArgs r = a;
+        r.W = a.Wf;
+        if (staged) launch_mf<GV_GEGLU, 2, 512, 4, 1, false, true>(s, r, 512, 1, nullptr);
+        else launch_mf<GV_GEGLU, 2, 512, 4, 1, true, true>(s, r, 512, 1, nullptr);
+        return;
+    }
+    if (staged) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
     else launch_mf<GV_GEGLU, 2, 512, 4, 1, true>(s, a, 512, 1, nullptr);  // input already normed
 }
 

@@ -92,6 +92,8 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
 // fused into the K-split combine (one workgroup per row)
 void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
                    float* ws, const uint16_t* norm_w, float eps, uint16_t* hn);
+// the fragment-major image of a [rows][K] matrix for the batched decode GEMVs (rows % 16 == 0, K % 32 == 0)
+void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out);
 // hn[b] = RMSNorm(x[b]) for nb rows of K (one workgroup per row)
 void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, int nb, int K, uint16_t* out);
 // o_proj + residual whose input is the combine of the decode-attention partials (MQA:
@@ -101,9 +103,10 @@ void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, i
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
                  const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq = nullptr);
 // fused RMSNorm + gate|up + GeGLU; ssq (B >= gemv_mf_min_batch() only): h's RMSNorm from the
-// partials gemv_o_attn wrote instead of the row pass
+// partials gemv_o_attn wrote instead of the row pass; Wf (idem): the gate|up weights' fragment-major
+// image (mf_swizzle: the gate rows', then the up rows'), read instead of Wgu
 void gemv_geglu(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
-                const uint16_t* Wgu, int I, uint16_t* act, float* ssq = nullptr);
+                const uint16_t* Wgu, int I, uint16_t* act, float* ssq = nullptr, const uint16_t* Wf = nullptr);
 int gemv_logits_blocks();
 int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 // done/next/adv (decode, may be null): fold the argmax into the launch's last workgroup and

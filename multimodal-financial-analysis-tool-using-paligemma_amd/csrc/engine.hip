@@ -103,9 +103,10 @@ struct pgmi_ctx {
     uint16_t *dH, *dQ, *dAO, *dACT;
     uint16_t* dHn;  // batched decode (B >= 3): the RMSNorm'd rows the unstaged MFMA projections read
     float* dSS;     // batched decode: o_proj's 16-column partial sums of squares of h, [B][H / 16]
-    // batched decode (max_batch >= 3): the fragment-major image of every layer's gate|up weights (mf_swizzle),
-    // [layer][2 I x H]
+    // batched decode (max_batch >= 3): fragment-major images of every layer's gate|up, q|k|v (in the GEMV's row
+    // order) and o_proj weights (mf_swizzle), [layer][gate|up 2 I x H | q|k|v QKVN x H | o_proj H x H]
     uint16_t* mfw = nullptr;
+    size_t mfw_layer = 0;
     float *opart, *pmax, *dlogits, *amax_v;
     int *pidx, *amax_i;
     int max_chunks;
@@ -632,10 +633,16 @@ int pgmi_prepare(pgmi_ctx* x) {
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
     LAUNCHCHK();
     if (c.max_batch >= gemv_mf_min_batch() && c.t_intermediate % 32 == 0 && c.t_hidden % 32 == 0) {
-        const size_t I = c.t_intermediate, H = c.t_hidden, per = 2 * I * H;
+        const size_t I = c.t_intermediate, H = c.t_hidden, QKVN = (size_t)(c.t_heads + 2 * c.t_kv_heads) * c.t_head_dim,
+                     OK = (size_t)c.t_heads * c.t_head_dim, per = 2 * I * H + QKVN * H + H * OK;
         if (!x->mfw && (rc = dalloc_t(x, &x->mfw, per * c.t_layers))) return rc;
-        for (int i = 0; i < c.t_layers; ++i)  // gate rows, then up rows (adjacent slots)
-            mf_swizzle(nullptr, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, x->mfw + per * i);
+        x->mfw_layer = per;
+        for (int i = 0; i < c.t_layers; ++i) {
+            uint16_t* L = x->mfw + per * i;
+            mf_swizzle(nullptr, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, L);  // gate rows, then up rows
+            mf_swizzle(nullptr, TL(x, i, "self_attn.q_proj.weight"), (int)QKVN, (int)H, L + 2 * I * H, true);  // q|k|v
+            mf_swizzle(nullptr, TL(x, i, "self_attn.o_proj.weight"), (int)H, (int)OK, L + 2 * I * H + QKVN * H);
+        }
         LAUNCHCHK();
     }
     std::vector<uint16_t> cs, sn;
@@ -977,9 +984,12 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     for (int i = 0; i < c.t_layers; ++i) {
         uint16_t* Kc = kvp + ((long)(i * 2 + 0) * kv_batch) * kvb;
         uint16_t* Vc = kvp + ((long)(i * 2 + 1) * kv_batch) * kvb;
+        // fragment-major weight images of this layer (prepare's mf_swizzle), when built: gate|up, q|k|v, o_proj
+        const uint16_t* Lf = x->mfw ? x->mfw + x->mfw_layer * i : nullptr;
+        const size_t gu_n = (size_t)2 * c.t_intermediate * H, qkv_n = (size_t)(NH + 2 * NKV) * HD * H;
         gemv_qkv(s, B, NH, NKV, mf ? x->dHn : x->dH, mf ? nullptr : TL(x, i, "input_layernorm.weight"), eps,
                  TL(x, i, "self_attn.q_proj.weight"), x->cosT, x->sinT, c.t_max_pos, x->step, x->dQ, Kc, Vc, kvb, x->ws,
-                 (fold && i == 0) ? &emb : nullptr);
+                 (fold && i == 0) ? &emb : nullptr, Lf ? Lf + gu_n : nullptr);
         AttnArgs a{};
         a.q = x->dQ; a.q_b_stride = (long)NH * HD; a.q_row_stride = NH * HD; a.q_head_stride = HD;
         a.k = Kc; a.k_b_stride = kvb; a.k_row_stride = (int)kvd; a.k_head_stride = HD;
@@ -993,12 +1003,10 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
         }
         attention_decode(s, a, x->step, launch_keys, x->opart, x->max_chunks);
         gemv_o_attn(s, B, NH, x->opart, x->max_chunks, x->step, TL(x, i, "self_attn.o_proj.weight"), H, x->dH,
-                    B >= gemv_mf_min_batch() ? x->dAO : nullptr, mf ? x->dSS : nullptr);
+                    B >= gemv_mf_min_batch() ? x->dAO : nullptr, mf ? x->dSS : nullptr, Lf ? Lf + gu_n + qkv_n : nullptr);
         if (mf) {
             // the post-attention RMSNorm: its sums of squares come from o_proj's epilogue (dSS), gate|up
             // normalises h on load (no k_rows_norm pass: B = 8 step -5 us per layer)
-            // gate|up from its fragment-major image (prepare's mf_swizzle), when built
-            const uint16_t* Lf = x->mfw ? x->mfw + (size_t)2 * c.t_intermediate * H * i : nullptr;
             gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                        c.t_intermediate, x->dACT, x->dSS, Lf);
             gemv_res_norm(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws,

@@ -35,7 +35,8 @@ bool gemv_qkv_folds_embed(int B) { return B <= 2 && B < gemv_mf_min_batch(); }
 
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
-              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws, const EmbedFold* emb) {
+              uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws, const EmbedFold* emb,
+              const uint16_t* Wf) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = Wqkv; a.n_units = (nh + 2 * nkv) * 128; a.K = 2048; a.nb = B;
     a.I = nh; a.out = q_out; a.cosT = cosT; a.sinT = sinT; a.max_pos = max_pos; a.st = st; a.kc = kc; a.vc = vc;
@@ -48,6 +49,7 @@ void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const ui
     }
 #define L_(b_, kch, rpw, mode) launch_gemv<b_, kch, rpw, mode>(s, a)
     if (B >= gemv_mf_min_batch()) {
+        a.Wf = Wf;
         gemv_mf_qkv(s, a, ws);
         return;
     }
@@ -96,12 +98,13 @@ void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_
 }
 
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
-                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq) {
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq, const uint16_t* Wf) {
     GemvArgs a{};
     a.x = nullptr; a.norm_w = nullptr; a.W = Wo; a.n_units = N; a.K = G * 256; a.nb = B; a.out = h_inout;
     a.part = part; a.max_chunks = max_chunks; a.G = G; a.st = st; a.o_out = o_out;
     if (B >= gemv_mf_min_batch() && o_out) {
         a.ssq = ssq;
+        a.Wf = N % 16 == 0 ? Wf : nullptr;
         gemv_mf_ores(s, a, o_out);
         return;
     }

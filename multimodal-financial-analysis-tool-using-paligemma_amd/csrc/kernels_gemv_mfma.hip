@@ -99,19 +99,26 @@ __device__ void mf_stage_rows(const GemvArgs& a, int K, uint16_t* xs, int ld, fl
 // (n = l & 15, g = l >> 4) holds row 16 g_row + n, k = 32 kb + 8 g .. + 8 -- so one load instruction of a
 // wave reads 1 KiB contiguous (the row-major image: 16 rows x 64 B, half lines whose other halves come one
 // instruction later).  Element offset of (row group gr, k block kb, lane l) = ((gr * K / 32 + kb) * 64 + l) * 8.
-__global__ void k_mf_swizzle(const uint16_t* __restrict__ W, int K, long n_chunks, uint16_t* __restrict__ out) {
+// qkv: the q|k|v GEMV's row order instead (k_gemv_mf<GV_QKV>: a 16-row group is 8 rotary pairs of one head).
+__device__ __forceinline__ long qkv_row(int u) {
+    const int grp_ = u >> 4, nn = u & 15;
+    return (long)((grp_ >> 4) * 256 + (grp_ & 15) * 8 + (nn & 7) + (nn >> 3) * 128);
+}
+
+__global__ void k_mf_swizzle(const uint16_t* __restrict__ W, int K, long n_chunks, int qkv, uint16_t* __restrict__ out) {
     const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 16-B chunk per thread
     if (c >= n_chunks) return;
     const int l = (int)(c & 63);
     const long blk = c >> 6, kbs = K / 32;
     const long gr = blk / kbs, kb = blk % kbs;
-    const long row = gr * 16 + (l & 15), k = kb * 32 + 8 * (l >> 4);
+    const int u = (int)(gr * 16 + (l & 15));
+    const long row = qkv ? qkv_row(u) : u, k = kb * 32 + 8 * (l >> 4);
     *reinterpret_cast<uint4*>(out + c * 8) = ldg16(W + row * K + k);
 }
 
-void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out) {
+void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out, bool qkv) {
     const long n = (long)rows * K / 8;
-    hipLaunchKernelGGL(k_mf_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, K, n, out);
+    hipLaunchKernelGGL(k_mf_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, K, n, (int)qkv, out);
 }
 
 // MODE: GV_*; NR: weight rows per unit (2: RoPE / GeGLU pairs); KW: K elements per wave; WK:
@@ -164,7 +171,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
     uint4 w[NR][NKB][4];
     // SW: the fragment-major image (k_mf_swizzle; n_units % 16 == 0, the up rows' image of n_groups groups
     // after the gate rows'): lane-linear 1-KiB pieces, k block stride 512 elements, read non-temporal
-    static_assert(!SW || MODE == GV_GEGLU, "fragment-major image: the gate|up GEMV");
+    static_assert(!SW || PF == 1, "fragment-major image: one-deep register streams");
     auto issue = [&](int grp) {
         int u = grp * 16 + n;
         if (u >= a.n_units) u = a.n_units - 1;  // clamp: duplicate row, result discarded
@@ -846,6 +853,12 @@ static int ms_blocks(int units, int cap) {
 void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
     GemvArgs r = a;
     r.n_units = 2 * a.n_units;
+    if (a.Wf) {  // the fragment-major weight image in the GEMV's row order (the decode step passes it)
+        r.W = a.Wf;
+        if (a.norm_w) launch_mf<GV_QKV, 1, 256, 8, 1, false, true>(s, r, groups_of(r.n_units), 1, nullptr);
+        else launch_mf<GV_QKV, 1, 256, 8, 1, true, true>(s, r, groups_of(r.n_units), 1, nullptr);
+        return;
+    }
     if (a.norm_w) launch_mf<GV_QKV, 1, 256, 8>(s, r, groups_of(r.n_units), 1, nullptr);
     else launch_mf<GV_QKV, 1, 256, 8, 1, true>(s, r, groups_of(r.n_units), 1, nullptr);  // input already normed
 }
@@ -881,6 +894,11 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
     // 128 workgroups of 8 waves splitting K (the q|k|v form) instead of 64 two-wave LDS-ring workgroups:
     // B = 8 step 1.751-1.760 -> 1.718-1.721 ms (same-box A/B).  (The same form for the K = 16384 down
     // projection, 1,024 workgroups, measured slower: 1.79 ms.)
+    if (a.Wf) {  // the fragment-major weight image (the decode step passes it)
+        r.W = a.Wf;
+        launch_mf<GV_RES, 1, 256, 8, 1, false, true>(s, r, groups_of(a.n_units), 1, nullptr);
+        return;
+    }
     launch_mf<GV_RES, 1, 256, 8>(s, r, groups_of(a.n_units), 1, nullptr);
 }
 

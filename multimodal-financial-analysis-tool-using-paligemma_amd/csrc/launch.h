@@ -84,7 +84,7 @@ bool gemv_qkv_folds_embed(int B);  // batches the fold covers (the register-inpu
 void gemv_qkv(hipStream_t s, int B, int nh, int nkv, const uint16_t* h, const uint16_t* norm_w, float eps,
               const uint16_t* Wqkv, const uint16_t* cosT, const uint16_t* sinT, int max_pos, const StepState* st,
               uint16_t* q_out, uint16_t* kc, uint16_t* vc, long kv_b_stride, float* ws = nullptr,
-              const EmbedFold* emb = nullptr);
+              const EmbedFold* emb = nullptr, const uint16_t* Wf = nullptr);  // Wf: as gemv_geglu's
 // ws: fp32 scratch (>= 4 x B x N floats) for the MFMA path's K split of K = 16384 (B >= 3)
 void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
               float* ws);
@@ -93,7 +93,8 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
 void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
                    float* ws, const uint16_t* norm_w, float eps, uint16_t* hn);
 // the fragment-major image of a [rows][K] matrix for the batched decode GEMVs (rows % 16 == 0, K % 32 == 0)
-void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out);
+// (qkv: in the batched q|k|v GEMV's row order)
+void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out, bool qkv = false);
 // hn[b] = RMSNorm(x[b]) for nb rows of K (one workgroup per row)
 void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, int nb, int K, uint16_t* out);
 // o_proj + residual whose input is the combine of the decode-attention partials (MQA:
@@ -101,7 +102,8 @@ void rows_norm(hipStream_t s, const uint16_t* x, const uint16_t* w, float eps, i
 // ssq (batched MFMA form only, else ignored): each row's 16-column partial sums of squares of the
 // new h, [B][N / 16] -- the next RMSNorm's, read by gemv_geglu
 void gemv_o_attn(hipStream_t s, int B, int G, const float* part, int max_chunks, const StepState* st,
-                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq = nullptr);
+                 const uint16_t* Wo, int N, uint16_t* h_inout, uint16_t* o_out, float* ssq = nullptr,
+                 const uint16_t* Wf = nullptr);
 // fused RMSNorm + gate|up + GeGLU; ssq (B >= gemv_mf_min_batch() only): h's RMSNorm from the
 // partials gemv_o_attn wrote instead of the row pass; Wf (idem): the gate|up weights' fragment-major
 // image (mf_swizzle: the gate rows', then the up rows'), read instead of Wgu

@@ -104,7 +104,7 @@ struct pgmi_ctx {
     uint16_t* dHn;  // batched decode (B >= 3): the RMSNorm'd rows the unstaged MFMA projections read
     float* dSS;     // batched decode: o_proj's 16-column partial sums of squares of h, [B][H / 16]
     // batched decode (max_batch >= 3): fragment-major images of every layer's gate|up, q|k|v (in the GEMV's row
-    // order) and o_proj weights (mf_swizzle), [layer][gate|up 2 I x H | q|k|v QKVN x H | o_proj H x H]
+    // order), o_proj and down weights (mf_swizzle), [layer][gate|up 2 I x H | q|k|v QKVN x H | o_proj | down H x I]
     uint16_t* mfw = nullptr;
     size_t mfw_layer = 0;
     float *opart, *pmax, *dlogits, *amax_v;
@@ -634,7 +634,7 @@ int pgmi_prepare(pgmi_ctx* x) {
     LAUNCHCHK();
     if (c.max_batch >= gemv_mf_min_batch() && c.t_intermediate % 32 == 0 && c.t_hidden % 32 == 0) {
         const size_t I = c.t_intermediate, H = c.t_hidden, QKVN = (size_t)(c.t_heads + 2 * c.t_kv_heads) * c.t_head_dim,
-                     OK = (size_t)c.t_heads * c.t_head_dim, per = 2 * I * H + QKVN * H + H * OK;
+                     OK = (size_t)c.t_heads * c.t_head_dim, per = 2 * I * H + QKVN * H + H * OK + H * I;
         if (!x->mfw && (rc = dalloc_t(x, &x->mfw, per * c.t_layers))) return rc;
         x->mfw_layer = per;
         for (int i = 0; i < c.t_layers; ++i) {
@@ -642,6 +642,7 @@ int pgmi_prepare(pgmi_ctx* x) {
             mf_swizzle(nullptr, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, L);  // gate rows, then up rows
             mf_swizzle(nullptr, TL(x, i, "self_attn.q_proj.weight"), (int)QKVN, (int)H, L + 2 * I * H, true);  // q|k|v
             mf_swizzle(nullptr, TL(x, i, "self_attn.o_proj.weight"), (int)H, (int)OK, L + 2 * I * H + QKVN * H);
+            mf_swizzle(nullptr, TL(x, i, "mlp.down_proj.weight"), (int)H, (int)I, L + 2 * I * H + QKVN * H + H * OK);
         }
         LAUNCHCHK();
     }
@@ -1010,7 +1011,8 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
             gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),
                        c.t_intermediate, x->dACT, x->dSS, Lf);
             gemv_res_norm(s, B, c.t_intermediate, x->dACT, TL(x, i, "mlp.down_proj.weight"), H, x->dH, x->ws,
-                          i + 1 < c.t_layers ? TL(x, i + 1, "input_layernorm.weight") : nullptr, eps, x->dHn);
+                          i + 1 < c.t_layers ? TL(x, i + 1, "input_layernorm.weight") : nullptr, eps, x->dHn,
+                          Lf ? Lf + gu_n + qkv_n + (size_t)H * NH * HD : nullptr);
             continue;
         }
         gemv_geglu(s, B, x->dH, TL(x, i, "post_attention_layernorm.weight"), eps, TL(x, i, "mlp.gate_proj.weight"),

@@ -86,10 +86,11 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
 // batched (MFMA) residual projection whose combine also writes the next RMSNorm of h (hn); other
 // batches / shapes: gemv_res, then rows_norm
 void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
-                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn) {
+                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn, const uint16_t* Wf) {
     if (B >= gemv_mf_min_batch() && K % 2048 == 0 && K / 2048 <= 8 && K > 2048 && ws) {
         GemvArgs a{};
         a.x = x; a.norm_w = nullptr; a.W = W; a.n_units = N; a.K = K; a.nb = B; a.out = h_inout;
+        a.Wf = N % 16 == 0 ? Wf : nullptr;
         gemv_mf_res_norm(s, a, ws, norm_w, eps, hn);
         return;
     }

@@ -913,7 +913,16 @@ int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2
 // combine: h (a.out) += down(x); hn = RMSNorm(h) with norm_w (nullptr: h only)
 void gemv_mf_res_norm(hipStream_t s, const GemvArgs& a, float* ws, const uint16_t* norm_w, float eps, uint16_t* hn) {
     const int KS = a.K / 2048;  // <= 8 (checked by the caller: gemv_res_norm)
-    launch_mf<GV_RES, 1, 512, 4, 2>(s, a, 32, KS, ws);
+    if (a.Wf) {
+        // the fragment-major image (the decode step passes it), one-deep streams: same box, B = 8 step
+        // 1.3461-1.3489 -> 1.3336-1.3339 ms against the two-deep row-major form below (the image with the
+        // two-deep streams read slower: profiles/r05_b8_fragment_image_ab.txt)
+        GemvArgs r = a;
+        r.W = a.Wf;
+        launch_mf<GV_RES, 1, 512, 4, 1, false, true>(s, r, 32, KS, ws);
+    } else {
+        launch_mf<GV_RES, 1, 512, 4, 2>(s, a, 32, KS, ws);
+    }
     hipLaunchKernelGGL(k_mf_combine_norm, dim3(a.nb), dim3(256), 0, s, ws, KS, a.n_units, a.out, norm_w, eps, hn);
 }
 

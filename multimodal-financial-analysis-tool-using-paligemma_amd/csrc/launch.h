@@ -91,7 +91,7 @@ void gemv_res(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W,
 // gemv_res, then hn = RMSNorm(h) with norm_w (nullptr: none); on the batched MFMA path the norm is
 // fused into the K-split combine (one workgroup per row)
 void gemv_res_norm(hipStream_t s, int B, int K, const uint16_t* x, const uint16_t* W, int N, uint16_t* h_inout,
-                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn);
+                   float* ws, const uint16_t* norm_w, float eps, uint16_t* hn, const uint16_t* Wf = nullptr);
 // the fragment-major image of a [rows][K] matrix for the batched decode GEMVs (rows % 16 == 0, K % 32 == 0)
 // (qkv: in the batched q|k|v GEMV's row order)
 void mf_swizzle(hipStream_t s, const uint16_t* W, int rows, int K, uint16_t* out, bool qkv = false);

@@ -864,7 +864,7 @@ void gemv_mf_qkv(hipStream_t s, const GemvArgs& a, float* /*ws*/) {
 }
 
 void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row pairs
-    // register-streamed MFMA form: 4 waves split K (512 each), 512 workgroups (2 per CU) dealing the
+    // register-streamed MFMA form: 4 waves split K (512 each); over the row-major weights 512 workgroups (2 per CU) dealing the
     // 1,024 row groups grid-stride, so each stages its 8 normalised rows for two groups; same-box A/B
     // (tools/b8_ab.sh) B = 8 step 1.737 -> 1.681 ms against the one-workgroup-per-CU LDS-DMA ring
     // (k_gemv_ml, 4 waves x 3-deep rings); 256 / 384 / 1,024 workgroups and 2 or 8 K-split waves
@@ -876,8 +876,10 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
     if (a.Wf) {
         GemvArgs r = a;
         r.W = a.Wf;
-        if (staged) launch_mf<GV_GEGLU, 2, 512, 4, 1, false, true>(s, r, 512, 1, nullptr);
-        else launch_mf<GV_GEGLU, 2, 512, 4, 1, true, true>(s, r, 512, 1, nullptr);
+        // 256 workgroups (one per CU, four groups each): same box, B = 8 step 1.3358-1.3376 ms at 512,
+        // 1.3300-1.3344 at 256, 1.3564-1.3573 at 384, 1.3667-1.3672 at 1,024 (profiles/r05_b8_grid_ab.txt)
+        if (staged) launch_mf<GV_GEGLU, 2, 512, 4, 1, false, true>(s, r, 256, 1, nullptr);
+        else launch_mf<GV_GEGLU, 2, 512, 4, 1, true, true>(s, r, 256, 1, nullptr);
         return;
     }
     if (staged) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);
@@ -916,7 +918,8 @@ void gemv_mf_res_norm(hipStream_t s, const GemvArgs& a, float* ws, const uint16_
     if (a.Wf) {
         // the fragment-major image (the decode step passes it), one-deep streams: same box, B = 8 step
         // 1.3461-1.3489 -> 1.3336-1.3339 ms against the two-deep row-major form below (the image with the
-        // two-deep streams read slower: profiles/r05_b8_fragment_image_ab.txt)
+        // two-deep streams read slower: profiles/r05_b8_fragment_image_ab.txt); 32 x 8 workgroups (64 / 16 x 8:
+        // 1.3574-1.3617 / 1.3514-1.3518 against 1.3374-1.3376, profiles/r05_b8_grid_ab.txt)
         GemvArgs r = a;
         r.W = a.Wf;
         launch_mf<GV_RES, 1, 512, 4, 1, false, true>(s, r, 32, KS, ws);

@@ -704,7 +704,8 @@ def main():
     torch.cuda.empty_cache()
     batch8 = None
     if world == 1 and not a.no_extra and B == 1:
-        batch8 = time_batch(cfg, dev, a.seed, g, 8, 64, 8)
+        # configs[3] at its stated length: 256 output tokens per image (SURVEY sec.8d cfg 4)
+        batch8 = time_batch(cfg, dev, a.seed, g, 8, 256, 8)
     api = None
     if world == 1 and not a.no_api and B == 1 and a.image_size == 224:
         api = time_api(cfg, dev, a.seed, a.api_tokens)

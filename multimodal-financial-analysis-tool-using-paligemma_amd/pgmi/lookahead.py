@@ -185,5 +185,10 @@ class GreedyLookahead:
 def lookahead_for(eng, B: int) -> GreedyLookahead:
     la = getattr(eng, "_lookahead", None)
     if la is None or la.B != B:
+        if la is not None and la.last is not None:
+            # the replaced lookahead's last step may still run on its side stream, in the engine's workspace:
+            # whatever the new one enqueues waits for it (its guard is replaced below)
+            torch.cuda.current_stream(eng.device).wait_event(la.last)
         la = eng._lookahead = GreedyLookahead(eng, B)
+        la.main_touched = True  # the first lookahead of the new object waits for the caller's stream
     return la

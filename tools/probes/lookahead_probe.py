@@ -97,6 +97,47 @@ def main():
         run(la)
     hits = getattr(getattr(eng, "_lookahead", None), "hits", None)
     print("lookahead hits", hits, "LA module", LA.__file__)
+    if os.environ.get("LA_PROBE_NOCHECK"):
+        # what the padding check's GPU ops (a side stream's compare + copy per token) cost the loop: the
+        # check replaced by nothing (probe only)
+        class _NoCheck:
+            def __init__(self, mask):
+                pass
+
+            def launch(self):
+                pass
+
+            def wait(self):
+                pass
+
+        MG._PaddingCheck = _NoCheck
+        print("# padding check off")
+        for la in (True, True):
+            run(la)
+    if os.environ.get("LA_PROBE_NOCLONE"):
+        # what the hit's logits copy on the caller's stream costs: the slot handed out as is (probe only -- the
+        # slot is rewritten three steps later)
+        def take_noclone(self, kv_cache, slab, cache_len, position, s, done, ne, graph, after_launch):
+            main = torch.cuda.current_stream(self.eng.device)
+            self.flag.copy_(ne, non_blocking=True)
+            self.ev_chk.record(main)
+            if after_launch is not None:
+                after_launch()
+            self._ahead(kv_cache, slab, cache_len + 1, position + 1, (s + 1) % LA.NSLOT, graph, False)
+            self.ev_chk.synchronize()
+            done.synchronize()
+            if not bool(self.flag):
+                kv_cache._pgmi_misses = 0
+                self.hits += 1
+                return self.logits[s].unsqueeze(1)
+            kv_cache._pgmi_misses = getattr(kv_cache, "_pgmi_misses", 0) + 1
+            self.pending = None
+            return None
+
+        LA.GreedyLookahead._take = take_noclone
+        print("# logits copy off")
+        for la in (True, True):
+            run(la)
 
 
 if __name__ == "__main__":

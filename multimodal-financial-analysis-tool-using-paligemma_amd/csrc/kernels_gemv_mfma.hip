@@ -274,6 +274,17 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
 #pragma unroll
         for (int c = 0; c < (FOLD ? Q4 / 4 : 1); ++c) sv[c] = sp[c];
     }
+    // unfolded, unstaged inputs: this wave's K slice of the rows before the stream, every load unconditional
+    // (rows n >= nb re-read row nb - 1: they only feed C rows b >= nb, never stored), so the first MFMA waits
+    // for its fragment only
+    if (!STAGE && !fold) {
+        const int row = n < a.nb ? n : a.nb - 1;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xf[kb][i] = __builtin_bit_cast(short8, ldg16(a.x + (long)row * K + k0 + kb * 128 + 32 * i + 8 * g));
+    }
     // unconditional (a workgroup past the last group streams that group again, unused): no branch around
     // the stream, so the waits for the loads above are counted past it
     issue(grp < n_groups ? grp : n_groups - 1);
@@ -321,13 +332,6 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 for (int j = 0; j < 8; ++j) o.v[j] = f2bf((bf2f(e.v[j]) * r) * (1.0f + bf2f(wv.v[j])));
                 xf[kb][i] = __builtin_bit_cast(short8, o);
             }
-    } else {
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                xf[kb][i] = n < a.nb ? __builtin_bit_cast(short8, ldg16(a.x + (long)n * K + k0 + kb * 128 + 32 * i + 8 * g))
-                                     : short8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 
     int kv_len = 0, pos = 0;
@@ -342,7 +346,13 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
 #pragma unroll
     for (int r = 0; r < 4; ++r) { best[r] = -INFINITY; besti[r] = 0x7fffffff; }
 
-    for (; grp < n_groups; grp += gridDim.x) {
+    // One trip per row group of the workgroup, the last one peeled off: the in-loop issue of the next group's
+    // stream is unconditional, so the compiler's in-order vmcnt model stays exact across trips and each MFMA
+    // waits for its own fragment (a branch around the issue made every trip wait vmcnt(0) for the whole stream
+    // before its first MFMA).  Same box, B = 8 step 1.3341 / 1.3282 / 1.3359 -> 1.3179 / 1.3021 / 1.3054 ms
+    // (profiles/r05_b8_peel_ab.txt)
+    auto body = [&](auto next_t) {
+        constexpr bool NEXT = decltype(next_t)::value;
         f32x4 acc[NR];
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
@@ -353,7 +363,8 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 for (int i = 0; i < 4; ++i) acc[j] = mfma16(xf[kb][i], __builtin_bit_cast(short8, w[j][kb][i]), acc[j]);
         }
         const int cur = grp;
-        if (grp + gridDim.x < n_groups) issue(grp + gridDim.x);  // next group's stream starts now
+        if constexpr (NEXT) issue(grp + gridDim.x);  // the next group's stream starts now (it exists)
+        grp += gridDim.x;
         if constexpr (WK > 1) {
 #pragma unroll
             for (int j = 0; j < NR; ++j) kred[wk][j][lane] = acc[j];
@@ -367,7 +378,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 }
             }
             __syncthreads();
-            if (wk != 0) continue;
+            if (wk != 0) return;
         }
         // C map: col n = unit (cur*16 + n), row b = 4g + r
         const int u = cur * 16 + n;
@@ -395,7 +406,7 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                     dst[d + hi * 128] = f2bf(hi ? x1 : x0);
                 }
             }
-            continue;
+            return;
         }
         if constexpr (MODE == GV_RES) {
             if (KS == 1) {
@@ -421,10 +432,10 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                         if (n == 0 && 4 * g + r < a.nb) a.ssq[(long)(4 * g + r) * n_groups + cur] = q[r];
                     }
                 }
-                continue;
+                return;
             }
         }
-        if (u >= a.n_units) continue;
+        if (u >= a.n_units) return;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int b = 4 * g + r;
@@ -441,7 +452,9 @@ __global__ void __launch_bounds__(64 * WK) k_gemv_mf(GemvArgs a, float* __restri
                 if (v > best[r]) { best[r] = v; besti[r] = u; }  // units visited in increasing order
             }
         }
-    }
+    };
+    while (grp + (int)gridDim.x < n_groups) body(std::true_type{});
+    if (grp < n_groups) body(std::false_type{});
     if constexpr (MODE == GV_LOGITS) {
         // first max per batch row over this workgroup's units: lanes of one g hold 16 columns
         __shared__ float bv[MF_MAXB];

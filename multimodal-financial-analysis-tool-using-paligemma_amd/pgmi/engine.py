@@ -77,6 +77,11 @@ class Engine:
     def __del__(self):
         try:
             if getattr(self, "ctx", None):
+                # a greedy lookahead step (pgmi/lookahead.py) may still run on its side stream in this context's
+                # workspace: it ends before the context's memory is released
+                la = self.__dict__.get("_lookahead")
+                if la is not None and la.last is not None:
+                    la.last.synchronize()
                 self.lib.pgmi_destroy(self.ctx)
                 self.ctx = None
         except Exception:

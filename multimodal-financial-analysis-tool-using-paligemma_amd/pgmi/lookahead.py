@@ -16,8 +16,10 @@ lookahead's logits out -- the caller's stream never waits on the side stream (a 
 slows the other queue's graphed step by ~0.09 ms: tools/probes/stream_probe.py, profiles/
 r05_stream_probe.txt), and nothing runs between two lookaheads on the side stream.
 Any other input (a sampled token, another position, another cache) runs the asked step on the caller's
-stream behind the lookahead, whose KV row lies past the cache's length and is overwritten.  After two misses in a row the lookahead stands down for that
-cache (a sampling loop, inference.py:64-66, would otherwise pay a wasted step per token).
+stream behind the lookahead, whose KV row lies past the cache's length and is overwritten.  A lookahead that is not
+asked for (the check fails, or the next call brings another cache or position) is a miss of its cache; after two
+misses in a row the lookahead stands down for that cache (a sampling loop, inference.py:64-66, or a loop that
+interleaves sequences would otherwise pay a wasted step per token).
 
 Ordering: the lookahead uses the engine's workspace and the cache's slab, so (1) the side stream waits for
 the caller's stream before a lookahead that follows a step (or any engine call) on the caller's stream --
@@ -116,6 +118,14 @@ class GreedyLookahead:
         self.pending = None
         return None
 
+    @staticmethod
+    def _wasted(p) -> None:
+        """The pending lookahead p was not asked for (another cache, position or batch came next): a miss of
+        its cache, so a loop that interleaves sequences stops paying a wasted step per token."""
+        c = p[0]()
+        if c is not None:
+            c._pgmi_misses = getattr(c, "_pgmi_misses", 0) + 1
+
     def step(self, kv_cache, slab, input_ids, cache_len: int, position: int, graph: bool, after_launch=None):
         """The logits (B, 1, V) of the decode step for input_ids at KV row cache_len / rotary `position`
         (a fresh tensor, as the reference returns); `after_launch` runs once the asked step is enqueued."""
@@ -124,8 +134,11 @@ class GreedyLookahead:
         p = self.pending
         self.pending = None
         s = 0
-        if (p is not None and p[0]() is kv_cache and p[1] == cache_len and p[2] == position
-                and ids.numel() == self.B):
+        if p is not None and not (p[0]() is kv_cache and p[1] == cache_len and p[2] == position
+                                  and ids.numel() == self.B):
+            self._wasted(p)
+            p = None
+        if p is not None:
             s = p[3]
             # the check on the caller's stream: the lookahead's input ids[s] was written by the step before
             # it, which the host has already waited for, so nothing here waits for the side stream
@@ -159,7 +172,10 @@ class GreedyLookahead:
         p = self.pending
         self.pending = None
         s = 0
-        if p is not None and p[0]() is kv_cache and p[1] == cache_len and ids.numel() == 1 == self.B:
+        if p is not None and not (p[0]() is kv_cache and p[1] == cache_len and ids.numel() == 1 == self.B):
+            self._wasted(p)
+            p = None
+        if p is not None:
             s = p[3]
             ne = torch.ne(ids, self.ids[s]).any()
             ne = ne | torch.ne(row.reshape(-1), embeds.reshape(-1)).any()

@@ -175,3 +175,42 @@ def test_lookahead_bit_identical_greedy_and_forced(model, G):
         ids = torch.topk(out["logits"][:, -1, :], 2, dim=-1).indices[:, 1:2]
         mask = torch.cat([mask, torch.ones((1, 1), device=ids.device)], dim=-1)
     assert la.hits == hits and la.pending is None
+
+
+@torch.no_grad()
+def test_lookahead_two_interleaved_caches(model, G):
+    """Two sequences decoded in alternation on one model (two KVCaches, greedy): every step finds the pending
+    lookahead on the other cache, runs behind it on the caller's stream and starts its own; each cache's
+    logits and KV rows equal those of the same alternation with the lookahead off, and the lookahead stands
+    down for both caches after two misses each."""
+    import modeling_gemma as MG
+    from pgmi.lookahead import lookahead_for
+    g = G["64"]
+    ids0 = torch.from_numpy(g["ids"]).cuda()
+    px = [torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda(),
+          torch.from_numpy(pixels_from_u8(G["px"]["u8_1_224"])[None]).cuda()]
+
+    def alternate(lookahead, n=12):
+        model.pgmi_lookahead = lookahead
+        try:
+            st = [{"ids": ids0, "mask": torch.ones_like(ids0), "kv": MG.KVCache(), "out": []} for _ in range(2)]
+            for t in range(n):
+                for j, s in enumerate(st):
+                    out = model(input_ids=s["ids"], pixel_values=px[j], attention_mask=s["mask"], kv_cache=s["kv"])
+                    lg = out["logits"][:, -1, :]
+                    s["out"].append(lg.clone())
+                    s["ids"] = torch.argmax(lg, dim=-1, keepdim=True)
+                    _ = int(s["ids"].item())
+                    s["mask"] = torch.cat([s["mask"], torch.ones((1, 1), device=lg.device)], dim=-1)
+            return st
+        finally:
+            model.pgmi_lookahead = True
+
+    on, off = alternate(True), alternate(False)
+    for a, b in zip(on, off):
+        assert torch.equal(torch.cat(a["out"]), torch.cat(b["out"]))
+        n = a["kv"].num_items()
+        assert n == b["kv"].num_items() == ids0.shape[1] + 11
+        assert torch.equal(a["kv"]._slab[:, :, :, :n], b["kv"]._slab[:, :, :, :n])
+        assert getattr(a["kv"], "_pgmi_misses", 0) >= 2
+    assert lookahead_for(model._pgmi_engine(), 1).pending is None

@@ -890,9 +890,12 @@ void gemv_mf_geglu(hipStream_t s, const GemvArgs& a) {  // K = 2048, gate|up row
         GemvArgs r = a;
         r.W = a.Wf;
         // 256 workgroups (one per CU, four groups each): same box, B = 8 step 1.3358-1.3376 ms at 512,
-        // 1.3300-1.3344 at 256, 1.3564-1.3573 at 384, 1.3667-1.3672 at 1,024 (profiles/r05_b8_grid_ab.txt)
+        // 1.3300-1.3344 at 256, 1.3564-1.3573 at 384, 1.3667-1.3672 at 1,024 (profiles/r05_b8_grid_ab.txt).
+        // Normalise-on-load form: 8 waves splitting K (256 each) once the loop was peeled -- same box, B = 8 step
+        // 1.3082 / 1.3089 / 1.3083 -> 1.3000 / 1.3002 / 1.2963 ms against 4 x 512 (512 workgroups 1.313, two-deep
+        // register streams 1.320, profiles/r05_b8_gu_waves_ab.txt)
         if (staged) launch_mf<GV_GEGLU, 2, 512, 4, 1, false, true>(s, r, 256, 1, nullptr);
-        else launch_mf<GV_GEGLU, 2, 512, 4, 1, true, true>(s, r, 256, 1, nullptr);
+        else launch_mf<GV_GEGLU, 2, 256, 8, 1, true, true>(s, r, 256, 1, nullptr);
         return;
     }
     if (staged) launch_mf<GV_GEGLU, 2, 512, 4>(s, a, 512, 1, nullptr);

@@ -921,7 +921,8 @@ void gemv_mf_ores(hipStream_t s, const GemvArgs& a, uint16_t* o) {
 }
 
 int gemv_mf_logits(hipStream_t s, const GemvArgs& a, int max_blocks) {  // K = 2048
-    // (the register-streamed form at 512 / 1,024 / 2,048 workgroups measured no faster: 1.741-1.768 ms)
+    // (the register-streamed form at 512 / 1,024 / 2,048 workgroups measured no faster: 1.741-1.768 ms; again in
+    // round 5 with the peeled loop: B = 8 step 1.283 -> 1.330-1.341 ms, profiles/r05_b8_lm_mf_ab.txt)
     const int blocks = ms_blocks(a.n_units, max_blocks < 256 ? max_blocks : 256);
     launch_ml<GV_LOGITS, 1, 2048, 6>(s, a, blocks, 1, nullptr);
     return blocks;
@@ -935,10 +936,13 @@ void gemv_mf_res_norm(hipStream_t s, const GemvArgs& a, float* ws, const uint16_
         // the fragment-major image (the decode step passes it), one-deep streams: same box, B = 8 step
         // 1.3461-1.3489 -> 1.3336-1.3339 ms against the two-deep row-major form below (the image with the
         // two-deep streams read slower: profiles/r05_b8_fragment_image_ab.txt); 32 x 8 workgroups (64 / 16 x 8:
-        // 1.3574-1.3617 / 1.3514-1.3518 against 1.3374-1.3376, profiles/r05_b8_grid_ab.txt)
+        // 1.3574-1.3617 / 1.3514-1.3518 against 1.3374-1.3376, profiles/r05_b8_grid_ab.txt); 8 waves of 256
+        // per K slice once the loop was peeled: 1.3003 / 1.2990 / 1.3016 -> 1.2855 / 1.2853 / 1.2807 ms against
+        // 4 waves of 512 (16 / 64 x 8 workgroups of 8 waves: 1.33 / 1.29; q|k|v and o_proj with 16 waves no faster;
+        // profiles/r05_b8_down_waves_ab.txt)
         GemvArgs r = a;
         r.W = a.Wf;
-        launch_mf<GV_RES, 1, 512, 4, 1, false, true>(s, r, 32, KS, ws);
+        launch_mf<GV_RES, 1, 256, 8, 1, false, true>(s, r, 32, KS, ws);
     } else {
         launch_mf<GV_RES, 1, 512, 4, 2>(s, a, 32, KS, ws);
     }

@@ -107,6 +107,7 @@ struct pgmi_ctx {
     // order), o_proj and down weights (mf_swizzle), [layer][gate|up 2 I x H | q|k|v QKVN x H | o_proj | down H x I]
     uint16_t* mfw = nullptr;
     size_t mfw_layer = 0;
+    bool mfw_dirty = false;  // the fragment-major images are (re)built by the next batched decode step
     float *opart, *pmax, *dlogits, *amax_v;
     int *pidx, *amax_i;
     int max_chunks;
@@ -632,20 +633,10 @@ int pgmi_prepare(pgmi_ctx* x) {
     pad_rows(nullptr, W(x, "vision_tower.vision_model.embeddings.patch_embedding.weight"), c.v_hidden,
              c.v_channels * c.v_patch * c.v_patch, x->kpad, x->patch_w);
     LAUNCHCHK();
-    if (c.max_batch >= gemv_mf_min_batch() && c.t_intermediate % 32 == 0 && c.t_hidden % 32 == 0) {
-        const size_t I = c.t_intermediate, H = c.t_hidden, QKVN = (size_t)(c.t_heads + 2 * c.t_kv_heads) * c.t_head_dim,
-                     OK = (size_t)c.t_heads * c.t_head_dim, per = 2 * I * H + QKVN * H + H * OK + H * I;
-        if (!x->mfw && (rc = dalloc_t(x, &x->mfw, per * c.t_layers))) return rc;
-        x->mfw_layer = per;
-        for (int i = 0; i < c.t_layers; ++i) {
-            uint16_t* L = x->mfw + per * i;
-            mf_swizzle(nullptr, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, L);  // gate rows, then up rows
-            mf_swizzle(nullptr, TL(x, i, "self_attn.q_proj.weight"), (int)QKVN, (int)H, L + 2 * I * H, true);  // q|k|v
-            mf_swizzle(nullptr, TL(x, i, "self_attn.o_proj.weight"), (int)H, (int)OK, L + 2 * I * H + QKVN * H);
-            mf_swizzle(nullptr, TL(x, i, "mlp.down_proj.weight"), (int)H, (int)I, L + 2 * I * H + QKVN * H + H * OK);
-        }
-        LAUNCHCHK();
-    }
+    // the batched decode's fragment-major weight images: built by the first decode step with B >= 3 after this
+    // call (ensure_mf_image), not here -- a context that never decodes a batch (the drop-in's single-sequence
+    // loop on its max_batch-8 context) neither allocates their 3.96 GB nor pays for the swizzle
+    x->mfw_dirty = c.max_batch >= gemv_mf_min_batch() && c.t_intermediate % 32 == 0 && c.t_hidden % 32 == 0;
     std::vector<uint16_t> cs, sn;
     if (!x->host_cos.empty()) {
         cs = x->host_cos;
@@ -1086,6 +1077,38 @@ struct DevStepIn {
     long mask_b_stride = 0;
 };
 
+// The fragment-major images of every layer's gate|up, q|k|v, o_proj and down weights that the batched (B >= 3)
+// decode projections read (kernels_gemv_mfma.hip; round 5), (re)built on stream s after a pgmi_prepare.  If the
+// 3.96 GB (at the 3B shapes) cannot be allocated the batched decode reads the row-major weights instead (the
+// same values in the same lanes: bit-identical results, slower), so the context stays usable.
+static int ensure_mf_image(pgmi_ctx* x, hipStream_t s) {
+    if (!x->mfw_dirty) return 0;
+    const pgmi_config& c = x->c;
+    const size_t I = c.t_intermediate, H = c.t_hidden, QKVN = (size_t)(c.t_heads + 2 * c.t_kv_heads) * c.t_head_dim,
+                 OK = (size_t)c.t_heads * c.t_head_dim, per = 2 * I * H + QKVN * H + H * OK + H * I;
+    x->mfw_dirty = false;
+    if (!x->mfw) {
+        void* p = nullptr;
+        if (hipMalloc(&p, per * c.t_layers * sizeof(uint16_t)) != hipSuccess) {
+            (void)hipGetLastError();  // out of memory: keep the row-major form
+            return 0;
+        }
+        x->allocs.push_back(p);
+        x->mfw = reinterpret_cast<uint16_t*>(p);
+        clear_dgraphs(x);  // steps captured before held the row-major launches
+    }
+    x->mfw_layer = per;
+    for (int i = 0; i < c.t_layers; ++i) {
+        uint16_t* L = x->mfw + per * i;
+        mf_swizzle(s, TL(x, i, "mlp.gate_proj.weight"), (int)(2 * I), (int)H, L);  // gate rows, then up rows
+        mf_swizzle(s, TL(x, i, "self_attn.q_proj.weight"), (int)QKVN, (int)H, L + 2 * I * H, true);  // q|k|v
+        mf_swizzle(s, TL(x, i, "self_attn.o_proj.weight"), (int)H, (int)OK, L + 2 * I * H + QKVN * H);
+        mf_swizzle(s, TL(x, i, "mlp.down_proj.weight"), (int)H, (int)I, L + 2 * I * H + QKVN * H + H * OK);
+    }
+    LAUNCHCHK();
+    return 0;
+}
+
 static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int B, void* kv, int kv_batch, int kv_max,
                        int kv_len, int position, float* logits, int64_t* next_ids, int use_graph, void* stream,
                        const DevStepIn* dev = nullptr) {
@@ -1097,6 +1120,7 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
     if ((!ids && !embeds) || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
+    if (B >= gemv_mf_min_batch() && (rc = ensure_mf_image(x, s))) return rc;
     int masked = 0;
     if (dev) {
         // position read on the device; the host no longer knows it, so the next call sets the state again

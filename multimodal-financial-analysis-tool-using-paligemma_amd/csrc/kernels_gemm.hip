@@ -714,7 +714,7 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
         const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
         // one row tile (n_mt == 1, flagged in bit 30 of code by launch_w): every weight byte is read by one
         // workgroup once, so those pieces stream non-temporal; the activation panel, which every workgroup
-        // re-reads, keeps the default policy.  Same box (tools/gpu_r4l.sh, the M = 288 gate|up): 43.1 / 43.8 /
+        // re-reads, keeps the default policy.  Same box (tools/archive/gpu_r4l.sh, the M = 288 gate|up): 43.1 / 43.8 /
         // 43.3 -> 41.2 / 41.7 / 41.4 us in situ, 224 px prefill 3.80 -> 3.77-3.79 ms
         const bool wnt = (code >> 30) & 1;
         auto issue = [&](int kt, int slot) {
@@ -775,7 +775,9 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
 #define PGMI_GEMM_W_PIPE 1
 #endif
     // (two fragment sets: taller wave tiles than TM 9 spill at three waves per SIMD)
-    constexpr bool PIPE = PGMI_GEMM_W_PIPE && TM <= 9 && EPI != EPI_ROPE;  // (RoPE epilogue: its operands spill)
+    // (and not when the accumulators plus two fragment sets pass ~200 registers: W144q's 144 accumulators)
+    constexpr bool PIPE = PGMI_GEMM_W_PIPE && TM <= 9 && EPI != EPI_ROPE &&  // (RoPE epilogue: its operands spill)
+                          2 * (TM + NB * TN) * 4 + NB * TM * TN * 4 <= 200;
     if constexpr (PIPE) {
     // Fragment reads pipelined across the barrier (k_gemm_p's schedule): per tile t,
     //   read kk=1 fragments of t | MFMAs kk=0 | lgkmcnt(0), barrier t+1 (tile t+1 landed; the loaders
@@ -1156,7 +1158,11 @@ enum Cfg : int {
     // 8-phase (k_gemm_8p): 2x4 waves, BN 256 (dual: 128 gate + 128 up), two K-tile buffers
     E256 = 36,     // TM 8: 256 rows
     E192 = 37,     // TM 6: 192 rows
-    kNumCfg = 38,
+    // round 6, M = 288 = 2 x 144 (no padded rows): one wave row of 9 MFMA row tiles
+    W144q = 38,    // 1x4 compute waves, TM 9, BN 256 (dual 128 + 128), 3 slots: 36 MFMAs per 13 fragment reads
+    W144h = 39,    // 1x4 compute waves, TM 9, BN 128 (dual 64 + 64),  4 slots
+    W144x8 = 40,   // 1x8 compute waves, TM 9, BN 256 (dual 128 + 128), 3 slots
+    kNumCfg = 41,
 };
 static_assert(kNumCfg == kGemmCfgs, "launch.h kGemmCfgs");
 
@@ -1197,8 +1203,8 @@ int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 144, 144, 144};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 256, 128, 256};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -1247,8 +1253,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {2304, 16384, 2048, true, E256, 1},     // text gate|up         261.8 us (W288w 301.8); in situ LM 10064 -> 9435 us
         {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 144, 144, 144};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 256, 128, 256};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (int i = 0; i < g_n_shape_plans; ++i) {
         const ShapePlan& o = g_shape_plans[i];
@@ -1297,7 +1303,7 @@ static int xcd_block(int n_mt, int n_nt, int S, int BM, int BN, int K) {
 
 static int xcd_block_pick(int n_mt, int n_nt, int S, int BM, int BN, int K) {
     const long G = (long)n_mt * n_nt * S;
-    // measured (same box, tools/gpu_r4c.sh): 8-image prefill 12.88 -> 12.59 ms, 448 px flat, but the
+    // measured (same box, tools/archive/gpu_r4c.sh): 8-image prefill 12.88 -> 12.59 ms, 448 px flat, but the
     // 224 px tower 1.46 -> 1.53 ms (its split-K fc2 picked a block order that reads fewer bytes and
     // runs slower): the block order is used for the batched prefills' activation panels (>= 2048 rows)
     if ((long)n_mt * BM < 2048) return 0;
@@ -1544,6 +1550,9 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case W128x64: launch_w<4, 2, 4, 2, 5, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case E256: launch_8p<8, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case E192: launch_8p<6, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W144q: launch_w<4, 1, 9, 4, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W144h: launch_w<4, 1, 9, 2, 4, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case W144x8: launch_w<8, 1, 9, 2, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         default: break;
     }
 #undef P_

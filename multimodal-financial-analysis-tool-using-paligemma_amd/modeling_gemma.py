@@ -332,13 +332,14 @@ class GemmaForCausalLM(nn.Module):
         """Forget the engine binding (after replacing Parameter objects; pgmi/binding.py)."""
         _binding.unbind(self)
 
-    def _pgmi_engine(self):
+    def _pgmi_engine(self, full_check: bool = False):
         owner = _binding.owner_of(self)
         if owner is not None:
-            return owner._pgmi_engine()
+            return owner._pgmi_engine(full_check)
         _check_tied(self)
         return _binding.bind(self, lambda: _binding.text_cfg(self.config), "language_model.",
-                             inv_freq=self.model.layers[0].self_attn.rotary_emb.inv_freq if self.model.layers else None)
+                             inv_freq=self.model.layers[0].self_attn.rotary_emb.inv_freq if self.model.layers else None,
+                             full_check=full_check)
 
     def forward(self, attention_mask: Optional[torch.Tensor] = None, position_ids: Optional[torch.LongTensor] = None,
                 inputs_embeds: Optional[torch.FloatTensor] = None, kv_cache: Optional[KVCache] = None, **kwargs) -> dict:
@@ -356,7 +357,7 @@ class GemmaForCausalLM(nn.Module):
             position_ids = torch.arange(L).unsqueeze(0)
         if not torch.is_tensor(attention_mask) or bool((attention_mask != 0).any()):
             return self._forward_masked(attention_mask, position_ids, inputs_embeds, kv_cache)
-        eng = self._pgmi_engine()
+        eng = self._pgmi_engine(full_check=kv_cache is None or kv_cache.num_items() == 0)
         pos = _positions_2d(position_ids, B, L)
         logits = _run_lm(eng, kv_cache, B, L, pos, embeds=inputs_embeds, logits_rows=kwargs.get("logits_rows", 0))
         out = {"logits": logits}
@@ -511,11 +512,12 @@ class PaliGemmaForConditionalGeneration(nn.Module):
         the current parameters into a new weight slab (pgmi/binding.py)."""
         _binding.unbind(self)
 
-    def _pgmi_engine(self):
+    def _pgmi_engine(self, full_check: bool = False):
         _check_tied(self.language_model)
         layers = self.language_model.model.layers
         return _binding.bind(self, lambda: _pgmi_cfg(self.config), "",
-                             inv_freq=layers[0].self_attn.rotary_emb.inv_freq if len(layers) else None)
+                             inv_freq=layers[0].self_attn.rotary_emb.inv_freq if len(layers) else None,
+                             full_check=full_check)
 
     def _merge_input_ids_with_image_features(self, image_features: torch.Tensor, inputs_embeds: torch.Tensor,
                                              input_ids: torch.Tensor, attention_mask: torch.Tensor,
@@ -575,9 +577,10 @@ class PaliGemmaForConditionalGeneration(nn.Module):
         if inputs_embeds is None and input_ids is None:
             chk.wait()
             raise ValueError("You must provide either input_ids or inputs_embeds")
-        eng = self._pgmi_engine()
-        dev = eng.device
         cache_len = kv_cache.num_items() if kv_cache is not None else 0
+        # a prefill also checks every weight the parameter sample cannot vouch for (pgmi/binding.py)
+        eng = self._pgmi_engine(full_check=cache_len == 0)
+        dev = eng.device
         src = input_ids if input_ids is not None else inputs_embeds
         B, L = src.shape[0], src.shape[1]
         mode = self.pgmi_prefill_logits

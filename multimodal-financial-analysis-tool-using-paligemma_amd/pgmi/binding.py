@@ -6,6 +6,12 @@ copy of the weights and later in-place updates (load_state_dict) land in the sla
 fingerprint (storage pointers and version counters of a parameter sample, the sampled Parameter
 objects kept from the first forward) detects .to(...) and in-place loads and rebuilds the engine;
 replacing Parameter objects needs an explicit unbind (pgmi_rebind on the top-level modules).
+At every prefill (full_check) the version counters of every parameter the sample cannot vouch for are
+checked too: the weights engine.prepare() derives tensors from (the text layers' projections -> the
+batched decode's fragment-major images, the patch embedding -> its padded copy) and any parameter that is
+not a slab view (its in-place update never reaches the slab).  A change there re-copies those parameters,
+drops the pending greedy lookahead and re-runs prepare() (round-6 verdict: an in-place update of an
+unsampled weight left the derived images and a pending lookahead stale).
 """
 from __future__ import annotations
 
@@ -51,15 +57,51 @@ def _inv_fingerprint(inv_freq):
     return None if inv_freq is None else (inv_freq.data_ptr(), inv_freq._version, inv_freq.dtype)
 
 
+# parameters engine.prepare() builds derived tensors from (csrc/engine.hip pgmi_prepare): the text layers'
+# projections (fragment-major images read by the batched decode) and the patch embedding (its padded copy)
+_DERIVED = ("self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight",
+            "self_attn.o_proj.weight", "mlp.gate_proj.weight", "mlp.up_proj.weight", "mlp.down_proj.weight")
+
+
+def _watched(name: str, p, view) -> bool:
+    """Checked at every prefill: a source of a derived tensor, or a parameter that is not a slab view."""
+    if p.data_ptr() != view.data_ptr():
+        return True
+    if "patch_embedding.weight" in name:
+        return True
+    return "language_model.model.layers." in name and name.endswith(_DERIVED)
+
+
+def _versions(watch):
+    return [(p.data_ptr(), p._version) for p, _ in watch]
+
+
 class _Bound:
-    def __init__(self, engine, sample, inv_fp):
+    def __init__(self, engine, sample, inv_fp, watch):
         self.engine, self.sample, self.fp, self.inv_fp = engine, sample, _fingerprint_of(sample), inv_fp
+        self.watch = watch  # [(parameter, slab view)] checked at every prefill
+        self.wfp = _versions(watch)
+
+    def refresh(self, inv_freq) -> None:
+        """An in-place update of a watched parameter: copy what is not a slab view, drop the pending greedy
+        lookahead (its logits came from the old weights), rebuild the derived tensors."""
+        eng = self.engine
+        with torch.no_grad():
+            for p, view in self.watch:
+                if p.data_ptr() != view.data_ptr():
+                    view.copy_(p.detach())
+        la = eng.__dict__.get("_lookahead")
+        if la is not None:
+            la.pending = None
+        eng.prepare(inv_freq=inv_freq)  # synchronises the device: a lookahead still running ends first
+        self.wfp = _versions(self.watch)
+        self.fp = _fingerprint_of(self.sample)
 
 
 _warned_dtypes = set()
 
 
-def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
+def bind(module, cfg: dict, prefix: str, inv_freq=None, full_check: bool = False) -> Engine:
     """Engine for `module` (parameters named prefix + local name in the slab).
 
     The binding is re-checked on every forward against a fingerprint of sampled parameters
@@ -67,6 +109,8 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
     The sampled parameter objects are kept, so the check costs ~17 attribute reads instead of a
     walk of the module tree (~0.4-0.8 ms per decode step at the 3B shapes); replacing Parameter
     objects after the first forward needs unbind(module) (PaliGemmaForConditionalGeneration.pgmi_rebind).
+    full_check (prefills): also compare the watched parameters' versions (module docstring), ~130 of them
+    at the 3B shapes (~15 us).
     `cfg` may be a callable returning the config dict (built only when an engine is built).  A bound
     module's device is its sampled parameters' (a move to another device re-points them: the
     fingerprint changes), so the per-forward check walks no module tree."""
@@ -78,11 +122,14 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
             # run_inference does, ablation_study_fixed.py:182): rebuild the RoPE table from its values
             b.engine.prepare(inv_freq=inv_freq)
             b.inv_fp = inv_fp
+        if full_check and _versions(b.watch) != b.wfp:
+            b.refresh(inv_freq)
         return b.engine
     dev = _device_of(module)
     if callable(cfg):
         cfg = cfg()
     eng = Engine(cfg, device=dev, max_batch=DEFAULT_MAX_BATCH, max_seq=DEFAULT_MAX_SEQ)
+    watch = []
     with torch.no_grad():
         for name, p in module.named_parameters():
             if p.is_floating_point() and p.dtype != torch.bfloat16 and p.dtype not in _warned_dtypes:
@@ -99,8 +146,10 @@ def bind(module, cfg: dict, prefix: str, inv_freq=None) -> Engine:
             view.copy_(p.detach())
             if p.dtype == torch.bfloat16 and p.device == dev:
                 p.data = view
+            if _watched(full, p, view):
+                watch.append((p, view))
     eng.prepare(inv_freq=inv_freq)
-    module.__dict__["_pgmi_bound"] = _Bound(eng, _sample(module), inv_fp)
+    module.__dict__["_pgmi_bound"] = _Bound(eng, _sample(module), inv_fp, watch)
     return eng
 
 
@@ -138,9 +187,9 @@ def vision_forward(transformer, pixel_values, prefix="vision_tower.vision_model.
     """SiglipVisionTransformer.forward (modeling_siglip.py:236-244) through pgmi_vision."""
     owner = owner_of(transformer)
     if owner is not None:
-        eng = owner._pgmi_engine()
+        eng = owner._pgmi_engine(full_check=True)  # the tower reads the padded patch matrix (a derived tensor)
     else:
-        eng = bind(transformer, vision_cfg(transformer.config), prefix)
+        eng = bind(transformer, vision_cfg(transformer.config), prefix, full_check=True)
     px = pixel_values
     if px.dtype not in (torch.float32, torch.bfloat16):
         px = px.float()

@@ -40,8 +40,12 @@ NSLOT = 3
 
 
 class GreedyLookahead:
+    """Held by its engine (Engine._lookahead, and Engine._stream_guard as a bound method); it refers back to
+    the engine weakly, so dropping the engine frees its context and memory at once, not at the next cyclic
+    garbage collection (Engine.__del__ first waits for the last lookahead step)."""
+
     def __init__(self, eng, B: int):
-        self.eng, self.B = eng, B
+        self._eng, self.B = weakref.ref(eng), B
         V = eng.cfgd["t_vocab"]
         dev = eng.device
         # slot s: ids[s] is the input token of the step whose logits go to logits[s]; that step's argmax goes
@@ -56,6 +60,13 @@ class GreedyLookahead:
         self.hits = 0
         self.main_touched = False  # an engine call ran on another stream since the last lookahead
         eng._stream_guard = self._guard
+
+    @property
+    def eng(self):
+        e = self._eng()
+        if e is None:
+            raise RuntimeError("the engine of this greedy lookahead has been released")
+        return e
 
     def _guard(self, handle) -> None:
         """Engine._s(): an engine call about to run on stream `handle` waits for the last lookahead (and the

@@ -29,35 +29,52 @@ from . import _native as N
 from .engine import Engine
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RES, EPI_RES, EPI_GEGLU = 0, 1, 2, 3, 4, 7
-_CTX: "OrderedDict" = OrderedDict()
+_CTX: "OrderedDict" = OrderedDict()   # (device, stream handle) -> (Engine, the torch stream)
 _CTX_MAX = 8  # contexts kept (least recently used evicted): callers that make streams per call stay bounded
+_RETIRED: list = []  # evicted contexts still possibly read by their stream: (event, Engine)
+
+
+def _reap() -> None:
+    """Free the evicted contexts whose stream has passed the event recorded at eviction."""
+    keep = []
+    for ev, e in _RETIRED:
+        if not ev.query():
+            keep.append((ev, e))
+    _RETIRED[:] = keep
 
 
 def _ctx(device: torch.device) -> Engine:
     """Context for the single-op entries on (device, current stream): a zero-layer model whose scratch
     (split-K partials, patch-embedding staging, attention partials) is used from offset 0 by every op,
     so ops issued on different streams get different contexts and never overwrite each other's.  At most
-    _CTX_MAX contexts are kept; an evicted one is freed once the device has drained."""
+    _CTX_MAX contexts are kept; an evicted one is freed once its stream has passed an event recorded at
+    eviction (no device-wide synchronisation in the middle of an op; nothing is evicted while the current
+    stream is being captured into a CUDA graph)."""
     dev = device.index if device.index is not None else torch.cuda.current_device()
-    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
-    e = _CTX.get(key)
-    if e is not None:
+    cur = torch.cuda.current_stream(dev)
+    key = (dev, cur.cuda_stream)
+    hit = _CTX.get(key)
+    if hit is not None:
         _CTX.move_to_end(key)
-    if e is None:
+        return hit[0]
+    capturing = torch.cuda.is_current_stream_capturing()
+    if not capturing:
+        _reap()
         while len(_CTX) >= _CTX_MAX:
-            (odev, _), old = _CTX.popitem(last=False)
-            # its scratch may still be read by kernels queued on its stream (which may itself be gone):
-            # drain the device before freeing (evictions are rare: one per stream past the bound)
-            torch.cuda.synchronize(odev)
-            del old
-        from .binding import _DUMMY_TEXT, _DUMMY_VISION
-        from .synthetic import init_policy
-        cfg = {"vision_config": dict(_DUMMY_VISION), "text_config": dict(_DUMMY_TEXT), "image_token_index": 7,
-               "projection_dim": 2048, "pad_token_id": None}
-        e = Engine(cfg, device=torch.device("cuda", dev), max_batch=1, max_seq=64, max_kv=64)
-        e.fill_synthetic(0, init_policy)
-        e.prepare()
-        _CTX[key] = e
+            _, (old, ostream) = _CTX.popitem(last=False)
+            # its scratch may still be read by kernels queued on its stream (torch streams are pooled, never
+            # destroyed, so the handle stays valid): freed once that stream passes this event
+            ev = torch.cuda.Event()
+            ev.record(ostream)
+            _RETIRED.append((ev, old))
+    from .binding import _DUMMY_TEXT, _DUMMY_VISION
+    from .synthetic import init_policy
+    cfg = {"vision_config": dict(_DUMMY_VISION), "text_config": dict(_DUMMY_TEXT), "image_token_index": 7,
+           "projection_dim": 2048, "pad_token_id": None}
+    e = Engine(cfg, device=torch.device("cuda", dev), max_batch=1, max_seq=64, max_kv=64)
+    e.fill_synthetic(0, init_policy)
+    e.prepare()
+    _CTX[key] = (e, cur)
     return e
 
 

@@ -645,17 +645,22 @@ def make_ablation_fp32():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation", "448decode", "r5"], default=None,
+    ap.add_argument("--only", choices=["batch8", "batch8_fp32", "long", "ablation", "448decode", "r5", "r6"], default=None,
                     help="generate only one later round's fixtures (full_batch8 / full256 / full_ablation)")
     a = ap.parse_args()
     torch.set_num_threads(8)
-    px = make_pixels() if a.only not in ("batch8", "batch8_fp32", "ablation", "r5") else None
+    px = make_pixels() if a.only not in ("batch8", "batch8_fp32", "ablation", "r5", "r6") else None
     if a.only == "r5":
         # round 5: fp32 truths for configs[2] (no-KV) and both modes of the ablation harness; configs[3]'s
         # batched rows at their stated 256 output tokens, with their fp32 truths
         make_nokv_fp32()
         make_ablation_fp32()
         make_batch_images(n_tokens=256)
+        make_batch_fp32()
+    elif a.only == "r6":
+        # round 6: configs[3]'s batched rows with the same 1,024 sampled vocabulary entries per step as every
+        # other full-size fixture (256 before), and their fp32 truths
+        make_batch_images(n_tokens=256, n_sample=N_SAMPLE_IDX)
         make_batch_fp32()
     elif a.only == "batch8":
         make_batch_images()

@@ -157,3 +157,64 @@ def test_submodule_forwards(model):
     assert y.shape == (1, 3, 2048) and y.dtype == torch.bfloat16 and bool(torch.isfinite(y.float()).all())
     z = layer.input_layernorm(x)
     assert z.shape == x.shape and bool(torch.isfinite(z.float()).all())
+
+
+def _greedy_logits(model, ids, px, B, steps=3):
+    """The reference loop (inference.py:55-78) at batch B (rows = the same image and prompt): the last-row
+    logits of the prefill and of `steps` greedy KV-cached steps, (B, steps + 1, V)."""
+    import modeling_gemma as MG
+    idsB, pxB = ids.expand(B, -1).contiguous(), px.expand(B, -1, -1, -1).contiguous()
+    kv, mask = MG.KVCache(), torch.ones_like(idsB)
+    out = model(input_ids=idsB, pixel_values=pxB, attention_mask=mask, kv_cache=kv)
+    res = [out["logits"][:, -1].float().clone()]
+    for _ in range(steps):
+        nxt = torch.argmax(res[-1], -1, keepdim=True)
+        mask = torch.cat([mask, torch.ones((B, 1), device=mask.device, dtype=mask.dtype)], -1)
+        res.append(model(input_ids=nxt, attention_mask=mask, kv_cache=kv)["logits"][:, -1].float().clone())
+    return torch.stack(res, 1)
+
+
+@torch.no_grad()
+def test_inplace_update_of_unsampled_weight_rebinds(gold):
+    """An in-place update of a weight the binding's parameter sample does not hold (a text layer's q_proj)
+    between two generations: the next prefill sees it (pgmi/binding.py full_check), drops the pending greedy
+    lookahead and rebuilds the derived tensors -- the batched decode's fragment-major images among them -- so
+    B = 1 and B = 8 logits equal those of a freshly bound model with the same weights (ablation_study_fixed.py
+    :304-332 updates a bound model in place with load_state_dict)."""
+    cfg = W.small_config()
+    m = _model(cfg)
+    ids, px = _inputs(gold)
+    _greedy_logits(m, ids, px, 1)
+    _greedy_logits(m, ids, px, 8)  # binds, builds the batched images, leaves a lookahead pending
+    sampled = {id(p) for p in m.__dict__["_pgmi_bound"].sample}
+    name, p = next((n, p) for n, p in m.named_parameters()
+                   if n.startswith("language_model.") and n.endswith("self_attn.q_proj.weight") and id(p) not in sampled)
+    p.mul_(0.5)
+    a1, a8 = _greedy_logits(m, ids, px, 1), _greedy_logits(m, ids, px, 8)
+    fresh = _model(cfg)
+    fresh.load_state_dict(m.state_dict())
+    fresh.tie_weights()
+    b1, b8 = _greedy_logits(fresh, ids, px, 1), _greedy_logits(fresh, ids, px, 8)
+    assert torch.equal(a1, b1), (name, (a1 - b1).abs().max().item())
+    assert torch.equal(a8, b8), (name, (a8 - b8).abs().max().item())
+    del fresh
+
+
+@torch.no_grad()
+def test_dropped_model_releases_engine_without_gc(gold):
+    """A model dropped after lookahead decode steps frees its engine (context, weight slab, workspaces) at
+    once: the greedy lookahead refers to its engine weakly, so no reference cycle waits for the collector."""
+    import gc
+    import weakref
+    m = _model(W.small_config())
+    ids, px = _inputs(gold)
+    lg = _greedy_logits(m, ids, px, 1)
+    eng = weakref.ref(m.__dict__["_pgmi_bound"].engine)
+    assert eng() is not None and eng().__dict__.get("_lookahead") is not None
+    gc.collect()
+    gc.disable()
+    try:
+        del m, lg
+        assert eng() is None
+    finally:
+        gc.enable()

@@ -2,7 +2,7 @@
 # Round-4 GPU check: parity tests of the touched areas (per-step rel-L2 records to
 # gpurun_out/parity_tests.jsonl), smoke, the default bench line, then a same-box A/B of the batched
 # (B = 8) decode step: the attention combine folded into the attention launch (PGMI_FUSED_COMB=1) or not.
-# usage (via gpurun): bash tools/gpu_r4a.sh [tests]
+# usage (via gpurun): bash tools/archive/gpu_r4a.sh [tests]
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

@@ -2,7 +2,7 @@
 # Round-4 full GPU pass: every -m gpu test (per-step parity records to gpurun_out/parity_tests.jsonl),
 # smoke, the default bench line, a same-box A/B of the batched (B = 8) attention combine fold, and the
 # rocprofv3 kernel-trace stats of a short bench run (profiles/r04_kernel_stats.csv).
-# usage (via gpurun): bash tools/gpu_r4b.sh
+# usage (via gpurun): bash tools/archive/gpu_r4b.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

@@ -2,7 +2,7 @@
 # Round-4 same-box A/Bs: prefill with the XCD block raster of the GEMMs (PGMI_GEMM_XBLK=1, default)
 # vs the run order (=0); B = 8 decode with the attention combine folded (PGMI_FUSED_COMB=1, default)
 # vs its own launch (=0); then the HBM probe (FETCH_SIZE / WRITE_SIZE per launch).
-# usage (via gpurun): bash tools/gpu_r4c.sh
+# usage (via gpurun): bash tools/archive/gpu_r4c.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

@@ -3,7 +3,7 @@
 # temporal load (libpgmi.so, PGMI_SMALL_NT=1) vs the streaming load (libpgmi_smallt.so), and the
 # o_proj workgroup cap (PGMI_ORES_CAP 256 default vs 128 / 64); then the default prefill/batched line
 # with the XCD block raster limited to >= 2048-row GEMMs and the combine launch unfolded.
-# usage (via gpurun): bash tools/gpu_r4d.sh
+# usage (via gpurun): bash tools/archive/gpu_r4d.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

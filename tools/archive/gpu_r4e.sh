@@ -2,7 +2,7 @@
 # Round-4 probe: B = 1 decode with part of each layer's gate|up weights read into the Infinity Cache
 # ahead of the GEGLU GEMV (PGMI_PF, engine.hip pf_cfg): serial (1) and on a forked side stream (2)
 # at several fractions / grid sizes, then kernel traces of PF=1 and PF=2 (timestamps show overlap).
-# usage (via gpurun): bash tools/gpu_r4e.sh
+# usage (via gpurun): bash tools/archive/gpu_r4e.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

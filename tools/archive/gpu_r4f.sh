@@ -2,7 +2,7 @@
 # Round-4 same-box sweep of the B = 1 streaming GEMVs: grid caps and two weight groups in flight
 # (PGMI_B1_<GU|DN|LM>_<CAP|D2>, kernels_gemv.hip), then the full-size teacher-forced parity test
 # with every two-deep form on.
-# usage (via gpurun): bash tools/gpu_r4f.sh
+# usage (via gpurun): bash tools/archive/gpu_r4f.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4: 448 px decode parity (new fixture), then B = 8 decode on v_dot2 GEMVs over RMSNorm'd rows
 # (PGMI_B8_DOT=1, PGMI_MF_STAGED=0) vs the MFMA kernels: same-box bench pairs and the batched parity test.
-# usage (via gpurun): bash tools/gpu_r4h.sh
+# usage (via gpurun): bash tools/archive/gpu_r4h.sh
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 closing evidence after the last Python changes (csrc unchanged since tools/gpu_r5final.sh, so its
+# Round 5 closing evidence after the last Python changes (csrc unchanged since tools/archive/gpu_r5final.sh, so its
 # per-kernel profile and pmc_traffic.json still match): every -m gpu test with the parity records, smoke(), and
 # the default bench line (config4 at 256 steps).  Each step under its own limit.
 set -e

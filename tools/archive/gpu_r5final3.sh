@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 closing evidence, second half (tools/gpu_r5final.sh's tests, smoke and bench ran on these sources; its
+# Round 5 closing evidence, second half (tools/archive/gpu_r5final.sh's tests, smoke and bench ran on these sources; its
 # MFMA-busy pass crashed in the profiler at start-up, before the program ran): the per-kernel trace and HBM passes
 # for this csrc digest (the prefill GEMMs' MFMA-busy record r05_kernel_pmc_mfma.csv predates only decode-GEMV
 # changes), then the bench line again with pmc_traffic.json matching the build.

@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from oracle import weights as W
-from tests_helpers import pixels_from_u8
+from tests_helpers import check_model_parity, pixels_from_u8
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 SEED = 1234
@@ -30,7 +30,8 @@ def rel(a, b):
 @pytest.fixture(scope="module")
 def G(golden_dir):
     load = lambda n: np.load(os.path.join(golden_dir, n))  # noqa: E731
-    return {"256": load("full256_bf16.npz"), "64": load("full_bf16.npz"), "px": load("pixels.npz")}
+    return {"256": load("full256_bf16.npz"), "64": load("full_bf16.npz"), "64f": load("full_fp32.npz"),
+            "px": load("pixels.npz")}
 
 
 @pytest.fixture(scope="module")
@@ -101,30 +102,64 @@ def test_prefill_all_row_logits_full_vocab(model, G):
     _check_rows(eager[0], g)
 
 
-@torch.no_grad()
-def test_inference_loop_full_size(model, G):
-    """inference.py:55-78 through the drop-in module, 64 greedy tokens vs the reference's."""
+def _dropin_loop(model, G, n=64, forced=None):
+    """inference.py:55-78 through the drop-in module (pixel_values re-passed, the float mask column appended,
+    argmax of logits[:, -1, :], .item() per token; the greedy lookahead on, as by default).  forced: feed these
+    tokens instead of the argmax (teacher forcing on the reference's path).  Returns the tokens chosen, the
+    sampled logits of every step (the fixture's 1,024 vocabulary entries) and the cache."""
     import modeling_gemma as MG
     g = G["64"]
     ids = torch.from_numpy(g["ids"]).cuda()
     px = torch.from_numpy(pixels_from_u8(G["px"]["u8_0_224"])[None]).cuda()
+    sidx = torch.from_numpy(g["sample_idx"]).cuda()
     mask = torch.ones_like(ids)
     kv = MG.KVCache()
-    toks = []
-    for _ in range(64):
+    toks, vals = [], []
+    for t in range(n):
         out = model(input_ids=ids, pixel_values=px, attention_mask=mask, kv_cache=kv)
         kv = out["kv_cache"]
-        nxt = torch.argmax(out["logits"][:, -1, :], dim=-1, keepdim=True)
+        last = out["logits"][:, -1, :]
+        vals.append(last[0, sidx].clone())
+        nxt = torch.argmax(last, dim=-1, keepdim=True)
         assert nxt.size() == (1, 1)
         nxt = nxt.squeeze(0)
         toks.append(int(nxt.item()))
+        if forced is not None:
+            nxt = torch.tensor([int(forced[t])], device=ids.device)
         ids = nxt.unsqueeze(-1)
         mask = torch.cat([mask, torch.ones((1, 1), device=ids.device)], dim=-1)
+    return np.array(toks), torch.stack(vals).cpu().numpy(), kv
+
+
+@torch.no_grad()
+def test_inference_loop_full_size(model, G):
+    """inference.py:55-78 through the drop-in module, 64 greedy tokens vs the reference's, and every step's
+    logits (through the lookahead's hits) held to SURVEY sec.8c's per-step rule against full_bf16.npz and its
+    fp32 truth, up to the first step where the free-running tokens may part (the reference indecisive)."""
+    g, f = G["64"], G["64f"]
+    toks, vals, kv = _dropin_loop(model, G)
     ref = g["tokens"].reshape(-1)
-    diff = np.nonzero(np.array(toks) != ref)[0]
+    diff = np.nonzero(toks != ref)[0]
+    upto = 64
     if len(diff):
         assert g["margin"][diff[0]] < 0.25, (diff[0], toks[:diff[0] + 2], ref[:diff[0] + 2])
+        upto = int(diff[0]) + 1  # the step that chose the other token still ran on the reference's prefix
+    check_model_parity("dropin_loop_free", vals[:upto], g["sample_vals"][:upto], f["sample_vals"][:upto])
     assert kv.num_items() == g["ids"].shape[1] + 63
+
+
+@torch.no_grad()
+def test_inference_loop_teacher_forced_full_size(model, G):
+    """The same loop fed the reference's own tokens (so every step runs on the reference's path): all 64 steps'
+    logits held to the per-step rule against full_bf16.npz and full_fp32.npz, with the greedy lookahead handing
+    back the steps whose token it predicted (the reference's token equals our argmax wherever it is decisive)."""
+    from pgmi.lookahead import lookahead_for
+    g, f = G["64"], G["64f"]
+    la = lookahead_for(model._pgmi_engine(), 1)
+    hits = la.hits
+    toks, vals, _ = _dropin_loop(model, G, forced=g["tokens"].reshape(-1))
+    check_model_parity("dropin_loop_teacher_forced", vals, g["sample_vals"], f["sample_vals"])
+    assert lookahead_for(model._pgmi_engine(), 1).hits - hits >= 32
 
 
 @torch.no_grad()

@@ -38,25 +38,22 @@ def main():
             f.write(co)
             f.flush()
             notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", f.name], capture_output=True, text=True).stdout
-        cur = {}
+        entries, cur = [], None
         for line in notes.splitlines():
-            m = re.match(r"\s+\.(\w+):\s+(.*)", line)
-            if not m:
+            if line.strip().startswith("- .agpr_count:"):
+                cur = {"agpr": line.split(":")[1].strip()}
+                entries.append(cur)
                 continue
-            k, v = m.groups()
-            if k == "agpr_count":
-                cur = {"agpr": v}
-            elif k in ("group_segment_fixed_size", "private_segment_fixed_size", "sgpr_count", "vgpr_count",
-                       "vgpr_spill_count", "sgpr_spill_count"):
-                cur[k] = v
-            elif k == "name" and cur:
-                cur["name"] = v
-                if sub in v and not v.endswith(".kd"):
-                    dem = subprocess.run(["c++filt", v], capture_output=True, text=True).stdout.strip()
-                    print(f"vgpr {cur.get('vgpr_count')} agpr {cur.get('agpr')} spill {cur.get('vgpr_spill_count')} "
-                          f"scratch {cur.get('private_segment_fixed_size')} lds {cur.get('group_segment_fixed_size')}  {dem}")
-                cur = {}
-
+            m = re.match(r"\s+\.(\w+):\s+(.*)", line)
+            if m and cur is not None and m.group(1) in ("name", "group_segment_fixed_size", "private_segment_fixed_size",
+                                                        "vgpr_count", "vgpr_spill_count", "sgpr_count"):
+                cur.setdefault(m.group(1), m.group(2))
+        for e in entries:
+            v = e.get("name", "")
+            if sub in v:
+                dem = subprocess.run(["c++filt", v], capture_output=True, text=True).stdout.strip()
+                print(f"vgpr {e.get('vgpr_count')} agpr {e.get('agpr')} spill {e.get('vgpr_spill_count')} "
+                      f"scratch {e.get('private_segment_fixed_size')} lds {e.get('group_segment_fixed_size')}  {dem}")
 
 if __name__ == "__main__":
     main()

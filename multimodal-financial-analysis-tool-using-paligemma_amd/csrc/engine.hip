@@ -1415,7 +1415,7 @@ int pgmi_tune_gemm_shape(int M, int N, int K, int dual, int cfg, int split) {
 }
 
 int pgmi_tune_attention(int variant) {
-    static const int ok[] = {-1, 0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94};
+    static const int ok[] = {-1, 0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94, 81, 82};
     for (int v : ok)
         if (v == variant) {
             attention_force_variant(variant);

@@ -1121,11 +1121,12 @@ static void launch_fs_t(hipStream_t s, const AttnArgs& a, int ns, int tps, dim3 
     hipLaunchKernelGGL((k_attn_fs<HD, NW, LW, ST, P2>), grid, dim3(64 * (NW + LW)), lds, s, a, ns, tps);
 }
 
-template <int HD>
+template <int HD, int NWQ = 0>
 static void launch_fs(hipStream_t s, const AttnArgs& a, int want_ns) {
     // head dim 256: 4 compute waves (their registers fit 2 waves per SIMD with the loaders, not 3) and a
-    // 5-slot ring (160 KiB); head dim 72: 8 compute waves, 8 slots
-    constexpr int NW = HD == 256 ? 4 : 8, LW = 4, ST = HD == 256 ? 5 : 8;
+    // 5-slot ring (160 KiB); head dim 72: 8 compute waves, 8 slots.  NWQ > 0: that many compute waves (fewer
+    // query rows per workgroup, more workgroups over the same keys: probe variants 81 / 82)
+    constexpr int NW = NWQ > 0 ? NWQ : HD == 256 ? 4 : 8, LW = 4, ST = HD == 256 ? 5 : 8;
     const int nrows = a.Lq * a.G, nt = (a.Lk + 31) / 32;
     int ns = fs_splits(a, HD, NW * 16, want_ns);
     const int tps = (nt + ns - 1) / ns;
@@ -1198,6 +1199,11 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         //   (tools/probes/plan_sweep.py --batch 8, whole tower) k_attn_fs: tower 4204 -> 3835 us
         const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
         v = head_dim == 256 ? 9 : (a.Lk <= 256 && rows <= 4096) ? 7 : 9;
+    }
+    if ((v == 81 || v == 82) && head_dim == 256) {  // one pass, 1 / 2 compute waves per workgroup, one key range
+        if (v == 81) launch_fs<256, 1>(s, a, 1);
+        else launch_fs<256, 2>(s, a, 1);
+        return;
     }
     if (v == 9 || v == 91 || v == 92 || v == 94) {  // one pass, keys split over workgroups (auto / 1 / 2 / 4 ranges)
         const int want = v == 9 ? 0 : v - 90;

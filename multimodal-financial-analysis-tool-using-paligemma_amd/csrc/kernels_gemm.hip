@@ -1610,7 +1610,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         // language-model prefill timed per candidate, split partials reduced by the residual + RMSNorm)
         {288, 2048, 2048, false, W128x128, 4},  // text o_proj           LM -45 us vs W64x64 unsplit
         {288, 16384, 2048, true, W288n, 1},     // text gate|up (GeGLU)  LM -27 us vs W288w
-        {288, 2048, 16384, false, W128x128, 4}, // text down             LM -33 us vs W288n split 8
+        {288, 2048, 16384, false, W288n, 8},    // text down             round 6 in situ: LM -26 / -50 us vs W128x128
+                                                // split 4 on two boxes (gpurun_out r6b / r6e; round 3 had the opposite)
         // vision rows: round 3, in situ (tools/probes/plan_sweep.py: the whole tower timed per
         // candidate; split-K partials of out_proj / fc2 are reduced by the residual + LayerNorm kernel)
         {256, 3456, 1152, false, P64x64s4, 1},  // vision q|k|v          tower -17 us vs W64x64

@@ -214,7 +214,7 @@ def test_argmax_rows(eng, rows, V):
         assert torch.equal(got.cpu(), y[1:].view(rows, V).argmax(-1))
 
 
-@pytest.mark.parametrize("variant", [0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94])
+@pytest.mark.parametrize("variant", [0, 7, 8, 41, 42, 21, 22, 44, 24, 9, 91, 92, 94, 81, 82])
 @pytest.mark.parametrize("B,Lq,Lk,H,Hkv,d,scale", [
     (1, 256, 256, 16, 16, 72, 72 ** -0.5),     # SigLIP 224
     (3, 17, 5, 16, 16, 72, 72 ** -0.5),        # fewer keys than one tile

@@ -111,7 +111,7 @@ def main():
         for name in (a.shapes or "qkv,o,gateup,down").split(","):
             if name == "attn":
                 rows = []
-                for v in [9, 91, 92, 94, 8, 42]:
+                for v in [9, 91, 92, 94, 8, 42, 81, 82]:
                     N.check(eng.lib.pgmi_tune_attention(v))
                     rows.append((time_lm(eng, args, a.iters)[0], v))
                 N.check(eng.lib.pgmi_tune_attention(-1))

@@ -210,9 +210,9 @@ def test_batch8_fp32_fixture_consistency(golden_dir):
     shared = [col[int(c)] for c in f8["sample_idx"]]
     assert np.array_equal(f8["sample_vals"][0], f0["sample_vals"][:n, shared])
     assert np.array_equal(b8["sample_vals"][0], b0["sample_vals"][:n, shared])
-    for r in range(f8["sample_vals"].shape[0]):
-        e = np.mean([np.linalg.norm(b8["sample_vals"][r, t] - f8["sample_vals"][r, t]) /
-                     np.linalg.norm(f8["sample_vals"][r, t]) for t in range(f8["sample_vals"].shape[1])])
+    bv, fv = b8["sample_vals"], f8["sample_vals"]  # (an NpzFile decompresses an array on every key access)
+    for r in range(fv.shape[0]):
+        e = np.mean(np.linalg.norm(bv[r] - fv[r], axis=-1) / np.linalg.norm(fv[r], axis=-1))
         assert 1e-3 < e < 5e-2, (r, e)
 
 

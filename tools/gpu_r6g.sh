@@ -12,3 +12,5 @@ echo b8 done
 timeout -k 10 500 python -u tools/probes/plan_sweep.py --target lm --px 448 --shapes gateup,down --cfgs 36,37,41,46 \
     --splits 4,5,8 --iters 10 --rel-tol 5e-2 > $OUT/insitu_448.txt 2>&1
 echo 448 done
+timeout -k 10 300 python -u tools/probes/plan_sweep.py --target lm --shapes attn --iters 20 > $OUT/insitu_attn224.txt 2>&1
+echo attn done

@@ -1199,6 +1199,10 @@ void attention_prefill(hipStream_t s, int head_dim, const AttnArgs& a) {
         //   (tools/probes/plan_sweep.py --batch 8, whole tower) k_attn_fs: tower 4204 -> 3835 us
         const long rows = (long)a.Lq * a.G * a.n_kv * a.B;
         v = head_dim == 256 ? 9 : (a.Lk <= 256 && rows <= 4096) ? 7 : 9;
+        // round 6: Gemma at one 224 px image (288 queries x 8 heads, 288 keys: no key split, 36 workgroups of
+        // 4 compute waves) takes 2 compute waves per workgroup, 72 workgroups over the same keys: in situ LM
+        // prefill 2,408.7 -> 2,394.0 us (gpurun_out r6g, variant 82; 1 wave, 81: 2,396.0)
+        if (head_dim == 256 && (a.Lk + 31) / 32 < 16 && (rows + 31) / 32 <= 256) v = 82;
     }
     if ((v == 81 || v == 82) && head_dim == 256) {  // one pass, 1 / 2 compute waves per workgroup, one key range
         if (v == 81) launch_fs<256, 1>(s, a, 1);

@@ -654,7 +654,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_p(const uint16_t* __restric
 // stall, not the matrix pipe, set the k-step time).  One raw s_barrier per k-tile: before barrier t
 // every loader has counted its own DMA of tile t as landed (vmcnt), after it the loaders refill the
 // slot of tile t-1 (whose fragments every compute wave read before reaching barrier t).
-template <int NW, int WM, int TM, int TN, int NB, int ST, int LW, int EPI, bool SPLIT>
+template <int NW, int WM, int TM, int TN, int NB, int ST, int LW, int EPI, bool SPLIT, bool RL = false>
 __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __restrict__ A, int lda,
                                                           const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
                                                           int kt_per_split, EpiArgs ea, float* __restrict__ ws,
@@ -776,9 +776,102 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
 #endif
     // (two fragment sets: taller wave tiles than TM 9 spill at three waves per SIMD)
     // (and not when the accumulators plus two fragment sets pass ~200 registers: W144q's 144 accumulators)
-    constexpr bool PIPE = PGMI_GEMM_W_PIPE && TM <= 9 && EPI != EPI_ROPE &&  // (RoPE epilogue: its operands spill)
+    constexpr bool PIPE = !RL && PGMI_GEMM_W_PIPE && TM <= 9 && EPI != EPI_ROPE &&  // (RoPE: its operands spill)
                           2 * (TM + NB * TN) * 4 + NB * TM * TN * 4 <= 200;
-    if constexpr (PIPE) {
+    if constexpr (RL) {
+    // In-wave reload (round 6, the RL configurations: one compute wave per SIMD with a wide wave tile, so each
+    // fragment read feeds 2 NB TN MFMAs): one set of A fragments, each row tile's reloaded for the next 32-deep
+    // step right behind the MFMAs that read it, and two sets of B fragments (the next step's read first), so
+    // the step's later rows multiply while the next step's fragments land -- a single wave overlaps its own LDS
+    // reads with its MFMAs, which k_gemm_w's lock-stepped pairs of waves did not (the M = 288 gate|up's
+    // diagnostic builds: 33.5 us with no LDS-DMA at all for 15.4 us of MFMA issue).  Per tile t:
+    //   (t, 0) landed | read B (t, 1) | rows: MFMA (t, 0), read A (t, 1) | lgkmcnt(0), barrier t + 1 (tile t's
+    //   reads are done: the loaders refill its slot) | read B (t + 1, 0) | rows: MFMA (t, 1), read A (t + 1, 0)
+    static_assert(EPI != EPI_ROPE, "in-wave reload: no RoPE epilogue");
+    short8 fa[TM], fbA[NB][TN], fbB[NB][TN];
+#define PGMI_R_CH(KK) (((((KK) * 4) + (lane >> 4)) ^ swz) << 4)
+#define PGMI_R_A(I, SB, KK) fa[I] = *reinterpret_cast<const short8*>((SB) + arow0 + (I) * 16 * 128 + PGMI_R_CH(KK))
+#define PGMI_R_B(FB, SB, KK)                                                                                \
+    do {                                                                                                    \
+        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
+            FB[b_][j_] = *reinterpret_cast<const short8*>((SB) + brow0 + (b_ * BN + j_ * 16) * 128 + PGMI_R_CH(KK)); \
+    } while (0)
+#define PGMI_R_ROW(I, FB)                                                                                   \
+    do {                                                                                                    \
+        if constexpr (PGMI_GEMM_DIAG & 1) {                                                                 \
+            asm volatile("" ::"v"(fa[I]));                                                                  \
+        } else {                                                                                            \
+            _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
+                acc[b_][I][j_] = mfma16(fa[I], FB[b_][j_], acc[b_][I][j_]);                                 \
+        }                                                                                                   \
+    } while (0)
+#define PGMI_R_DIAGB(FB)                                                                                    \
+    do {                                                                                                    \
+        if constexpr (PGMI_GEMM_DIAG & 1) {                                                                 \
+            _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
+                asm volatile("" ::"v"(FB[b_][j_]));                                                         \
+        }                                                                                                   \
+    } while (0)
+    int slot = 0;
+    if (nkt > 0) {
+        __builtin_amdgcn_s_barrier();  // tile 0 is in slot 0
+#pragma unroll
+        for (int i = 0; i < TM; ++i) PGMI_R_A(i, smem_w, 0);
+        PGMI_R_B(fbA, smem_w, 0);
+    }
+    // every tile but the last (no branch inside the step: a step with and one without the reloads as two arms
+    // of one loop body made hipcc copy the accumulators between register assignments and spill)
+    for (int t = 0; t + 1 < nkt; ++t) {
+        const uint8_t* sb = smem_w + slot * SBYTES;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (t, 0)'s fragments
+        __builtin_amdgcn_sched_barrier(0);
+        PGMI_R_B(fbB, sb, 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            PGMI_R_ROW(i, fbA);
+            PGMI_R_A(i, sb, 1);
+            __builtin_amdgcn_sched_barrier(0);  // the reload stays behind the MFMAs that read fa[i]
+        }
+        PGMI_R_DIAGB(fbA);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // (t, 1)'s fragments: every read of tile t has landed
+        __builtin_amdgcn_sched_barrier(0);
+        slot = slot + 1 == ST ? 0 : slot + 1;
+        const uint8_t* nb = smem_w + slot * SBYTES;
+        __builtin_amdgcn_s_barrier();        // tile t + 1 landed; the loaders may refill tile t's slot
+        __builtin_amdgcn_sched_barrier(0);
+        PGMI_R_B(fbA, nb, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            PGMI_R_ROW(i, fbB);
+            PGMI_R_A(i, nb, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        PGMI_R_DIAGB(fbB);
+    }
+    if (nkt > 0) {  // the last tile
+        const uint8_t* sb = smem_w + slot * SBYTES;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        PGMI_R_B(fbB, sb, 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            PGMI_R_ROW(i, fbA);
+            PGMI_R_A(i, sb, 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        PGMI_R_DIAGB(fbA);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) PGMI_R_ROW(i, fbB);
+        PGMI_R_DIAGB(fbB);
+    }
+#undef PGMI_R_CH
+#undef PGMI_R_A
+#undef PGMI_R_B
+#undef PGMI_R_ROW
+#undef PGMI_R_DIAGB
+    } else if constexpr (PIPE) {
     // Fragment reads pipelined across the barrier (k_gemm_p's schedule): per tile t,
     //   read kk=1 fragments of t | MFMAs kk=0 | lgkmcnt(0), barrier t+1 (tile t+1 landed; the loaders
     //   may now refill t's slot: its fragments are all in registers) | read kk=0 fragments of t+1 |
@@ -876,379 +969,6 @@ __global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_w(const uint16_t* __
             }
     } else if constexpr (EPI == EPI_ROPE) {
         rope_apply<TM>(ea, M, m0 + wm * TM * 16, lane, rope_ops, acc[0]);
-    } else {
-        epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
-    }
-}
-
-// ---------------------------------------------------------------- warp-specialised GEMM, 32-deep ring (round 6)
-// k_gemm_w with ring slots of 32-deep k steps instead of 64: the same LDS holds twice as many slots, so the
-// loaders keep about twice the bytes in flight per CU (the prefill GEMMs run at the ~40 GB/s of L2 -> LDS
-// intake per CU that one to two 64-deep slots in flight allow; the LDS-DMA engine reaches ~68 GB/s with more,
-// MI355X_MICROARCH.md ring-gemm).  A slot row is 64 B: a 1-KiB DMA piece is 16 rows x 64 B (lane l: row l >> 2,
-// 16-B chunk l & 3), the chunk XOR-ed with (row >> 2) & 3 on the source address, so the 16 lanes of a
-// ds_read_b128 group (16 rows, one chunk) hit 16 distinct 16-B slots of a 256-B bank row.  One barrier per
-// slot: before barrier t every loader has counted its DMA of step t landed, after it the loaders refill the
-// slot of step t - 1; a compute wave reads step t + 1's fragments right after barrier t + 1 and multiplies step
-// t's (read before that barrier) meanwhile.  K tails (K % 32) read the zero chunk.
-template <int NW, int WM, int TM, int TN, int NB, int ST, int LW, int EPI, bool SPLIT>
-__global__ void __launch_bounds__(64 * (NW + LW), 1) k_gemm_h(const uint16_t* __restrict__ A, int lda,
-                                                          const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
-                                                          int kt_per_split, EpiArgs ea, float* __restrict__ ws,
-                                                          long up_off, int n_mt, int code) {
-    constexpr int WN = NW / WM;
-    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
-    static_assert(BM % 16 == 0 && BN % 16 == 0, "16-row pieces");
-    constexpr int APC = BM / 16, BPC = NB * BN / 16;  // 1-KiB pieces per 32-deep slot
-    constexpr int PCS = APC + BPC;
-    constexpr int GPW = (PCS + LW - 1) / LW;
-    constexpr int ABYTES = BM * 64;
-    constexpr int SBYTES = (BM + NB * BN) * 64;
-    static_assert(ST >= 3, "ring of at least three slots");
-    static_assert(EPI != EPI_ROPE, "no RoPE epilogue");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_h[];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int mt, nt, z;
-    xcd_tile(n_mt, code, mt, nt, z);
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int nkt_total = (K + 31) / 32;
-    const int kt0 = z * kt_per_split;
-    int kt1 = kt0 + kt_per_split;
-    if (kt1 > nkt_total) kt1 = nkt_total;
-    const int nkt = kt1 > kt0 ? kt1 - kt0 : 0;
-
-    if (wave >= NW) {
-        // ---------------- loader wave
-        const int lw = wave - NW;
-        const uint16_t* src[GPW];
-        int gk[GPW], loff[GPW];
-        const int prow = lane >> 2;
-        const int gch = (lane & 3) ^ ((lane >> 4) & 3);  // global chunk of the lane's LDS chunk (row >> 2 & 3)
-#pragma unroll
-        for (int i = 0; i < GPW; ++i) {
-            int p = lw + LW * i;
-            if (p >= PCS) p -= PCS;  // padding: repeat a piece (same bytes to the same LDS address)
-            loff[i] = p * 1024;
-            int row;
-            const uint16_t* base;
-            long ld;
-            if (p < APC) {
-                row = m0 + p * 16 + prow;
-                if (row > M - 1) row = M - 1;
-                base = A;
-                ld = lda;
-            } else {
-                const int q = p - APC;
-                const int bo = q / (BN / 16);
-                row = n0 + (q % (BN / 16)) * 16 + prow;
-                if (row > N - 1) row = N - 1;
-                base = W + bo * up_off;
-                ld = ldw;
-            }
-            gk[i] = gch * 8;
-            src[i] = base + (long)row * ld + gk[i];
-        }
-        const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-        auto issue = [&](int kt, int slot) {
-            if constexpr (PGMI_GEMM_DIAG & 2) return;
-            const int kel = kt * 32;
-            if (kel + 32 <= K) {
-#pragma unroll
-                for (int i = 0; i < GPW; ++i)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
-                                                     (__attribute__((address_space(3))) void*)(smem_h + slot * SBYTES + loff[i]),
-                                                     16, 0, 0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < GPW; ++i) {
-                    const uint16_t* g = (kel + gk[i] < K) ? src[i] + kel : zero;
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
-                                                     (__attribute__((address_space(3))) void*)(smem_h + slot * SBYTES + loff[i]),
-                                                     16, 0, 0);
-                }
-            }
-        };
-#pragma unroll
-        for (int sI = 0; sI < ST - 1; ++sI)
-            if (sI < nkt) issue(kt0 + sI, sI);
-        int slot_next = ST - 1;  // slot of step t + ST - 1
-        for (int t = 0; t < nkt; ++t) {
-            const int issued = (nkt < t + ST - 1) ? nkt : t + ST - 1;
-            vm_wait_tiles<GPW, ST - 2>(issued - t - 1);  // step t landed
-            __builtin_amdgcn_s_barrier();
-            if (t + ST - 1 < nkt) issue(kt0 + t + ST - 1, slot_next);
-            slot_next = slot_next + 1 == ST ? 0 : slot_next + 1;
-        }
-        return;
-    }
-
-    // ---------------- compute wave
-    const int wm = wave / WN, wn = wave % WN;
-    f32x4 acc[NB][TM][TN];
-#pragma unroll
-    for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[bb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // fragment rows are 16-aligned + (lane & 15): (row >> 2) & 3 == (lane >> 2) & 3
-    const int ch = ((lane >> 4) ^ ((lane >> 2) & 3)) << 4;
-    const int arow0 = (wm * TM * 16 + (lane & 15)) * 64 + ch;
-    const int brow0 = ABYTES + (wn * TN * 16 + (lane & 15)) * 64 + ch;
-    // one set of fragments, each reloaded for the next step right behind the MFMAs that read it (A row tile by
-    // row tile, B once all of the step's MFMAs are issued): the next step's fragments land while this step's
-    // later rows multiply, in the registers of one set (two whole sets do not fit beside TM 9 x 2 accumulator
-    // tiles at three waves per SIMD)
-    short8 fa[TM], fb[NB][TN];
-#define PGMI_H_READ_A(I, SLOT) \
-    fa[I] = *reinterpret_cast<const short8*>(smem_h + (SLOT) * SBYTES + arow0 + (I) * 16 * 64)
-#define PGMI_H_READ_B(SLOT)                                                                                 \
-    do {                                                                                                    \
-        _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
-            fb[b_][j_] = *reinterpret_cast<const short8*>(smem_h + (SLOT) * SBYTES + brow0 + (b_ * BN + j_ * 16) * 64); \
-    } while (0)
-#define PGMI_H_ROW(I)                                                                                       \
-    do {                                                                                                    \
-        if constexpr (PGMI_GEMM_DIAG & 1) {                                                                 \
-            asm volatile("" ::"v"(fa[I]));                                                                  \
-        } else {                                                                                            \
-            _Pragma("unroll") for (int b_ = 0; b_ < NB; ++b_) _Pragma("unroll") for (int j_ = 0; j_ < TN; ++j_) \
-                acc[b_][I][j_] = mfma16(fa[I], fb[b_][j_], acc[b_][I][j_]);                                 \
-        }                                                                                                   \
-    } while (0)
-    // step t's fragments were read after barrier t; barrier t + 1 (step t + 1 landed, and step t's slot may be
-    // refilled: every read of it has landed, lgkmcnt(0)) comes before step t's MFMAs
-    if (nkt > 0) {
-        __builtin_amdgcn_s_barrier();  // barrier 0: step 0 is in slot 0
-#pragma unroll
-        for (int i = 0; i < TM; ++i) PGMI_H_READ_A(i, 0);
-        PGMI_H_READ_B(0);
-    }
-    int slot = 0;
-    for (int t = 0; t + 1 < nkt; ++t) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): step t's fragments are in
-        slot = slot + 1 == ST ? 0 : slot + 1;
-        __builtin_amdgcn_s_barrier();        // barrier t + 1
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            PGMI_H_ROW(i);
-            PGMI_H_READ_A(i, slot);
-            __builtin_amdgcn_sched_barrier(0);  // the reload stays behind the MFMAs that read fa[i]
-        }
-        if constexpr (PGMI_GEMM_DIAG & 1) {
-#pragma unroll
-            for (int b_ = 0; b_ < NB; ++b_)
-#pragma unroll
-                for (int j_ = 0; j_ < TN; ++j_) asm volatile("" ::"v"(fb[b_][j_]));
-        }
-        PGMI_H_READ_B(slot);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (nkt > 0) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // the last step
-#pragma unroll
-        for (int i = 0; i < TM; ++i) PGMI_H_ROW(i);
-    }
-#undef PGMI_H_READ_A
-#undef PGMI_H_READ_B
-#undef PGMI_H_ROW
-    if constexpr (SPLIT) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
-                }
-            }
-    } else {
-        epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
-    }
-}
-
-// ---------------------------------------------------------------- warp-specialised ping-pong GEMM (round 6)
-// k_gemm_w's tiles, ring and loader waves, with its 8 compute waves split into two groups of 4 (group g =
-// waves 4g .. 4g+3: one wave of each group per SIMD) that run staggered: every 32-deep k step (a "phase",
-// two per k-tile) is READ fragments | s_barrier | MFMA cluster | s_barrier, and group 1 runs one barrier behind
-// group 0, so on each SIMD one wave multiplies while its partner reads (cdna_hip_programming.md's 8-phase
-// ping-pong; in k_gemm_w both waves of a SIMD read and multiply in lock step).  Barrier g0 of the launch is the
-// prologue's (tile 0 landed); group 0's phase P sits between barriers 2P+1 and 2P+2, group 1's between 2P+2 and
-// 2P+3.  The loaders count tile u landed before barrier 4u (read first in group 0's phase 2u, after barrier 4u)
-// and refill tile t's slot with tile t + ST after barrier 4t + 5 (group 1's reads of tile t, its phase 2t + 1,
-// are retired by the lgkmcnt(0) it waits after barrier 4t + 4).  4 nkt + 2 barriers for every wave.
-template <int WM, int TM, int TN, int NB, int ST, int EPI, bool SPLIT>
-__global__ void __launch_bounds__(64 * 12, 1) k_gemm_wp(const uint16_t* __restrict__ A, int lda,
-                                                      const uint16_t* __restrict__ W, int ldw, int M, int N, int K,
-                                                      int kt_per_split, EpiArgs ea, float* __restrict__ ws,
-                                                      long up_off, int n_mt, int code) {
-    constexpr int NW = 8, LW = 4;
-    constexpr int WN = NW / WM;
-    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
-    constexpr int APC = BM / 8, BPC = NB * BN / 8;  // 1-KiB pieces per k-tile
-    constexpr int PCS = APC + BPC;
-    constexpr int GPW = (PCS + LW - 1) / LW;
-    constexpr int ABYTES = BM * 128;
-    constexpr int SBYTES = (BM + NB * BN) * 128;
-    static_assert(ST >= 2, "ring of at least two slots");
-    static_assert(EPI != EPI_ROPE, "no RoPE epilogue");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_wp[];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int mt, nt, z;
-    xcd_tile(n_mt, code, mt, nt, z);
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int nkt_total = (K + 63) / 64;
-    const int kt0 = z * kt_per_split;
-    int kt1 = kt0 + kt_per_split;
-    if (kt1 > nkt_total) kt1 = nkt_total;
-    const int nkt = kt1 > kt0 ? kt1 - kt0 : 0;
-    const int nbar = 4 * nkt + 2;
-
-    if (wave >= NW) {
-        // ---------------- loader wave
-        const int lw = wave - NW;
-        const uint16_t* src[GPW];
-        int gk[GPW], loff[GPW];
-        const int prow = lane >> 3, pchunk = lane & 7;
-#pragma unroll
-        for (int i = 0; i < GPW; ++i) {
-            int p = lw + LW * i;
-            if (p >= PCS) p -= PCS;
-            loff[i] = p * 1024;
-            int row;
-            const uint16_t* base;
-            long ld;
-            if (p < APC) {
-                row = m0 + p * 8 + prow;
-                if (row > M - 1) row = M - 1;
-                base = A;
-                ld = lda;
-            } else {
-                const int q = p - APC;
-                const int bo = q / (BN / 8);
-                row = n0 + (q % (BN / 8)) * 8 + prow;
-                if (row > N - 1) row = N - 1;
-                base = W + bo * up_off;
-                ld = ldw;
-            }
-            gk[i] = (pchunk ^ (row & 7)) * 8;
-            src[i] = base + (long)row * ld + gk[i];
-        }
-        const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-        const bool wnt = (code >> 30) & 1;
-        auto issue = [&](int kt, int slot) {
-            if constexpr (PGMI_GEMM_DIAG & 2) return;
-            const int kel = kt * 64;
-            if (kel + 64 <= K) {
-#pragma unroll
-                for (int i = 0; i < GPW; ++i) {
-                    const int p = lw + LW * i < PCS ? lw + LW * i : lw + LW * i - PCS;
-                    if (wnt && p >= APC)
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
-                                                         (__attribute__((address_space(3))) void*)(smem_wp + slot * SBYTES + loff[i]),
-                                                         16, 0, 2);
-                    else
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + kel),
-                                                         (__attribute__((address_space(3))) void*)(smem_wp + slot * SBYTES + loff[i]),
-                                                         16, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < GPW; ++i) {
-                    const uint16_t* g = (kel + gk[i] < K) ? src[i] + kel : zero;
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
-                                                     (__attribute__((address_space(3))) void*)(smem_wp + slot * SBYTES + loff[i]),
-                                                     16, 0, 0);
-                }
-            }
-        };
-#pragma unroll
-        for (int sI = 0; sI < ST; ++sI)
-            if (sI < nkt) issue(kt0 + sI, sI);
-        int issued = nkt < ST ? nkt : ST;  // tiles issued so far
-        for (int b = 0; b < nbar; ++b) {
-            if ((b & 3) == 0) {
-                const int u = b >> 2;  // tile u landed before barrier 4u (u = 0: the prologue's barrier)
-                if (u < nkt) vm_wait_tiles<GPW, ST - 1>(issued - u - 1);
-            }
-            __builtin_amdgcn_s_barrier();
-            if (b >= 5 && ((b - 5) & 3) == 0) {
-                const int t = (b - 5) >> 2;  // every read of tile t is retired: its slot takes tile t + ST
-                if (t + ST < nkt) {
-                    issue(kt0 + t + ST, t % ST);
-                    ++issued;
-                }
-            }
-        }
-        return;
-    }
-
-    // ---------------- compute wave
-    const int grp = wave >> 2;
-    const int wm = wave / WN, wn = wave % WN;
-    f32x4 acc[NB][TM][TN];
-#pragma unroll
-    for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[bb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int swz = lane & 7;
-    const int arow0 = (wm * TM * 16 + (lane & 15)) * 128;
-    const int brow0 = ABYTES + (wn * TN * 16 + (lane & 15)) * 128;
-    short8 fa[TM], fb[NB][TN];
-    __builtin_amdgcn_s_barrier();                  // barrier 0: tile 0 landed
-    if (grp == 1) __builtin_amdgcn_s_barrier();    // group 1 runs one barrier behind
-    for (int P = 0; P < 2 * nkt; ++P) {
-        const int t = P >> 1, kk = P & 1;
-        const uint8_t* sb = smem_wp + (t % ST) * SBYTES;
-        const int ch = (((kk * 4) + (lane >> 4)) ^ swz) << 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const short8*>(sb + arow0 + i * 16 * 128 + ch);
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                fb[bb][j] = *reinterpret_cast<const short8*>(sb + brow0 + (bb * BN + j * 16) * 128 + ch);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        if constexpr (PGMI_GEMM_DIAG & 1) {
-            diag_consume<TM, TN, NB>(fa, fb);
-        } else {
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[bb][i][j] = mfma16(fa[i], fb[bb][j], acc[bb][i][j]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-    }
-    if (grp == 0) __builtin_amdgcn_s_barrier();    // the lagging group's last barrier
-    if constexpr (SPLIT) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + (wn * TN + j) * 16 + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = m0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + r;
-                    if (m < M && n < N) ws[((long)z * M + m) * N + n] = acc[0][i][j][r];
-                }
-            }
     } else {
         epi_tile<EPI, TM, TN>(ea, M, N, m0 + wm * TM * 16, n0 + wn * TN * 16, lane, acc[0], acc[NB - 1]);
     }
@@ -1533,23 +1253,9 @@ enum Cfg : int {
     // 8-phase (k_gemm_8p): 2x4 waves, BN 256 (dual: 128 gate + 128 up), two K-tile buffers
     E256 = 36,     // TM 8: 256 rows
     E192 = 37,     // TM 6: 192 rows
-    // round 6, M = 288 = 2 x 144 (no padded rows): one wave row of 9 MFMA row tiles
-    W144q = 38,    // 1x4 compute waves, TM 9, BN 256 (dual 128 + 128), 3 slots: 36 MFMAs per 13 fragment reads
-    W144h = 39,    // 1x4 compute waves, TM 9, BN 128 (dual 64 + 64),  4 slots
-    W144x8 = 40,   // 1x8 compute waves, TM 9, BN 256 (dual 128 + 128), 3 slots
-    // ping-pong (k_gemm_wp): 8 compute waves in two groups one barrier apart + 4 loader waves
-    V288n = 41,    // 2x4 compute waves, TM 9, BN 64 (dual 32 + 32): W288n's tiles
-    V288w = 42,    // 2x4 compute waves, TM 9, BN 128 (dual 64 + 64): W288w's tiles
-    V144x8 = 43,   // 1x8 compute waves, TM 9, BN 256 (dual 128 + 128)
-    V128x128 = 44, // 2x4 compute waves, TM 4, BN 128, 4 slots: W128x128's tiles
-    // 32-deep ring slots (k_gemm_h): twice the slots of the k_gemm_w tiles in the same LDS
-    H288n = 45,    // 2x4 compute waves, TM 9, BN 64 (dual 32 + 32), 6 slots
-    H288w = 46,    // 2x4 compute waves, TM 9, BN 128 (dual 64 + 64), 6 slots
-    H128x128 = 47, // 2x4 compute waves, TM 4, BN 128, 9 slots
-    H144x8 = 48,   // 1x8 compute waves, TM 9, BN 256 (dual 128 + 128), 6 slots
-    H64x64 = 49,   // 2x2 compute waves, TM 2, BN 64, 12 slots
-    H96x64 = 50,   // 2x2 compute waves, TM 3, BN 64, 10 slots (M = 288 = 3 x 96; vision rows)
-    kNumCfg = 51,
+    // round 6: k_gemm_w's in-wave reload mode (W288w's tiles; bit-identical results)
+    R288w = 38,    // 2x4 compute waves, TM 9, BN 128 (dual 64 + 64), 3 slots
+    kNumCfg = 39,
 };
 static_assert(kNumCfg == kGemmCfgs, "launch.h kGemmCfgs");
 
@@ -1590,8 +1296,8 @@ int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split) {
 
 static Plan choose(int M, int N, int K, bool dual) {
     if (g_force_cfg >= 0) {
-        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 144, 144, 144, 288, 288, 144, 128, 288, 288, 128, 144, 64, 96};
-        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 256, 128, 256, 64, 128, 256, 128, 64, 128, 128, 256, 64, 64};
+        static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 288};
+        static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 128};
         const int c = g_force_cfg;
         const int bn = (dual && c >= P288w) ? bns[c] / 2 : bns[c];
         return {(Cfg)c, bms[c], bn, dual && c < P288w ? 1 : (g_force_split > 0 ? g_force_split : 1)};
@@ -1609,7 +1315,9 @@ static Plan choose(int M, int N, int K, bool dual) {
         // text rows, round 3 in situ (tools/probes/plan_sweep.py --target lm: the generate loop's whole
         // language-model prefill timed per candidate, split partials reduced by the residual + RMSNorm)
         {288, 2048, 2048, false, W128x128, 4},  // text o_proj           LM -45 us vs W64x64 unsplit
-        {288, 16384, 2048, true, W288n, 1},     // text gate|up (GeGLU)  LM -27 us vs W288w
+        {288, 16384, 2048, true, R288w, 1},     // text gate|up (GeGLU)  LM -27 us vs W288w (round 3, W288n); round 6:
+                                                // the in-wave reload form of the same tiles, bit-identical, isolated
+                                                // 47.2 -> 40.5 us (cold), in situ -7 us per LM prefill (gpurun_out r6i)
         {288, 2048, 16384, false, W288n, 8},    // text down             round 6 in situ: LM -26 / -50 us vs W128x128
                                                 // split 4 on two boxes (gpurun_out r6b / r6e; round 3 had the opposite)
         // vision rows: round 3, in situ (tools/probes/plan_sweep.py: the whole tower timed per
@@ -1641,8 +1349,8 @@ static Plan choose(int M, int N, int K, bool dual) {
         {2304, 16384, 2048, true, E256, 1},     // text gate|up         261.8 us (W288w 301.8); in situ LM 10064 -> 9435 us
         {2304, 2048, 16384, false, W288w, 2},   // text down            153.9 us (was 298.6)
     };
-    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 144, 144, 144, 288, 288, 144, 128, 288, 288, 128, 144, 64, 96};
-    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 256, 128, 256, 64, 128, 256, 128, 64, 128, 128, 256, 64, 64};
+    static const int bms[] = {288, 288, 256, 256, 128, 128, 288, 256, 352, 288, 256, 128, 288, 256, 64, 128, 64, 128, 64, 128, 288, 352, 256, 288, 64, 64, 32, 64, 96, 96, 288, 288, 64, 352, 128, 128, 256, 192, 288};
+    static const int bns[] = {64, 32, 64, 32, 128, 64, 128, 128, 128, 64, 64, 128, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128, 128, 256, 64, 64, 64, 32, 64, 64, 128, 64, 64, 128, 128, 64, 256, 256, 128};
     auto mk = [&](Cfg c, int split) -> Plan { return {c, bms[c], dual ? bns[c] / 2 : bns[c], dual ? 1 : split}; };
     for (int i = 0; i < g_n_shape_plans; ++i) {
         const ShapePlan& o = g_shape_plans[i];
@@ -1823,8 +1531,8 @@ static void launch_p(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     }
 }
 
-// warp-specialised launcher: as launch_p, NW compute waves (grid WM x NW/WM) + LW loader waves
-template <int NW, int WM, int TM, int TNW, int ST, int LW, int EPI>
+// warp-specialised launcher: as launch_p, NW compute waves (grid WM x NW/WM) + LW loader waves (RL: in-wave reload)
+template <int NW, int WM, int TM, int TNW, int ST, int LW, int EPI, bool RL = false>
 static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
                      const EpiArgs& ea, float* ws, int split, long up_off) {
     constexpr bool DUAL = (EPI == EPI_GEGLU);
@@ -1841,15 +1549,15 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
     const int code = xcd_block(n_mt, n_nt, split, BM, NB * BN, K) | (n_mt == 1 ? 1 << 30 : 0);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false, RL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true, RL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
     const dim3 block(64 * (NW + LW));
     if (EPI < 0 || split > 1) {
-        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, true, RL>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, n_mt, code);
         if (EPI >= 0) {
             long total4 = ((long)M * N + 3) / 4;
@@ -1858,88 +1566,8 @@ static void launch_w(hipStream_t s, const uint16_t* A, int lda, const uint16_t* 
             hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
         }
     } else {
-        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
+        PGMI_GEMM_LAUNCH((k_gemm_w<NW, WM, TM, TN, NB, ST, LW, EK, false, RL>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
                            per, ea, ws, up_off, n_mt, code);
-    }
-}
-
-// 32-deep-slot launcher: as launch_w (kt_per_split counts 32-deep steps)
-template <int NW, int WM, int TM, int TNW, int ST, int LW, int EPI>
-static void launch_h(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
-                     const EpiArgs& ea, float* ws, int split, long up_off) {
-    constexpr bool DUAL = (EPI == EPI_GEGLU);
-    constexpr int NB = DUAL ? 2 : 1;
-    constexpr int TN = DUAL ? (TNW >= 2 ? TNW / 2 : 1) : TNW;
-    constexpr int BM = WM * TM * 16, BN = (NW / WM) * TN * 16;
-    constexpr size_t lds = (size_t)ST * (BM + NB * BN) * 64;
-    static_assert(lds <= 163840, "LDS ring exceeds 160 KiB");
-    constexpr int EK = EPI < 0 ? EPI_STORE : EPI;
-    const int nkt = (K + 31) / 32;
-    const int per = (nkt + split - 1) / split;
-    const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
-    dim3 grid(n_mt * n_nt, split);
-    const int code = xcd_block(n_mt, n_nt, split, BM, NB * BN, K);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_h<NW, WM, TM, TN, NB, ST, LW, EK, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_h<NW, WM, TM, TN, NB, ST, LW, EK, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-    }
-    const dim3 block(64 * (NW + LW));
-    if (EPI < 0 || split > 1) {
-        PGMI_GEMM_LAUNCH((k_gemm_h<NW, WM, TM, TN, NB, ST, LW, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                         per, ea, ws, up_off, n_mt, code);
-        if (EPI >= 0) {
-            long total4 = ((long)M * N + 3) / 4;
-            long blocks = (total4 + 255) / 256;
-            if (blocks > 4096) blocks = 4096;
-            hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
-        }
-    } else {
-        PGMI_GEMM_LAUNCH((k_gemm_h<NW, WM, TM, TN, NB, ST, LW, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K,
-                         per, ea, ws, up_off, n_mt, code);
-    }
-}
-
-// ping-pong launcher: as launch_w with 8 compute waves in two staggered groups + 4 loader waves
-template <int WM, int TM, int TNW, int ST, int EPI>
-static void launch_wp(hipStream_t s, const uint16_t* A, int lda, const uint16_t* W, int ldw, int M, int N, int K,
-                      const EpiArgs& ea, float* ws, int split, long up_off) {
-    constexpr bool DUAL = (EPI == EPI_GEGLU);
-    constexpr int NB = DUAL ? 2 : 1;
-    constexpr int TN = DUAL ? (TNW >= 2 ? TNW / 2 : 1) : TNW;
-    constexpr int BM = WM * TM * 16, BN = (8 / WM) * TN * 16;
-    constexpr size_t lds = (size_t)ST * (BM + NB * BN) * 128;
-    static_assert(lds <= 163840, "LDS ring exceeds 160 KiB");
-    constexpr int EK = EPI < 0 ? EPI_STORE : EPI;
-    const int nkt = (K + 63) / 64;
-    const int per = (nkt + split - 1) / split;
-    const int n_mt = (M + BM - 1) / BM, n_nt = (N + BN - 1) / BN;
-    dim3 grid(n_mt * n_nt, split);
-    const int code = xcd_block(n_mt, n_nt, split, BM, NB * BN, K) | (n_mt == 1 ? 1 << 30 : 0);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wp<WM, TM, TN, NB, ST, EK, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wp<WM, TM, TN, NB, ST, EK, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-    }
-    const dim3 block(64 * 12);
-    if (EPI < 0 || split > 1) {
-        PGMI_GEMM_LAUNCH((k_gemm_wp<WM, TM, TN, NB, ST, EK, true>), grid, block, lds, s, A, lda, W, ldw, M, N, K, per,
-                         ea, ws, up_off, n_mt, code);
-        if (EPI >= 0) {
-            long total4 = ((long)M * N + 3) / 4;
-            long blocks = (total4 + 255) / 256;
-            if (blocks > 4096) blocks = 4096;
-            hipLaunchKernelGGL((k_splitk_epi<EK>), dim3((unsigned)blocks), dim3(256), 0, s, ws, split, M, N, ea);
-        }
-    } else {
-        PGMI_GEMM_LAUNCH((k_gemm_wp<WM, TM, TN, NB, ST, EK, false>), grid, block, lds, s, A, lda, W, ldw, M, N, K, per,
-                         ea, ws, up_off, n_mt, code);
     }
 }
 
@@ -2018,19 +1646,7 @@ static void launch_pcfg(hipStream_t s, const uint16_t* A, int lda, const uint16_
         case W128x64: launch_w<4, 2, 4, 2, 5, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case E256: launch_8p<8, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         case E192: launch_8p<6, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case W144q: launch_w<4, 1, 9, 4, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case W144h: launch_w<4, 1, 9, 2, 4, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case W144x8: launch_w<8, 1, 9, 2, 3, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case V288n: launch_wp<2, 9, 1, 3, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case V288w: launch_wp<2, 9, 2, 3, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case V144x8: launch_wp<1, 9, 2, 3, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case V128x128: launch_wp<2, 4, 2, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H288n: launch_h<8, 2, 9, 1, 6, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H288w: launch_h<8, 2, 9, 2, 6, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H128x128: launch_h<8, 2, 4, 2, 9, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H144x8: launch_h<8, 1, 9, 2, 6, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H64x64: launch_h<4, 2, 2, 2, 12, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
-        case H96x64: launch_h<4, 2, 3, 2, 10, 4, EPI>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
+        case R288w: launch_w<8, 2, 9, 2, 3, 4, EPI, true>(s, A, lda, W, ldw, M, N, K, ea, ws, p.split, up_off); break;
         default: break;
     }
 #undef P_

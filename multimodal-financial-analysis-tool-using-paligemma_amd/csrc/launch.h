@@ -63,7 +63,7 @@ int gemm_force_shape(int M, int N, int K, int dual, int cfg, int split);  // cfg
 void gemm_probe_events(hipEvent_t start, hipEvent_t stop);
 // host replica of the panel / 8-phase GEMMs' workgroup -> tile order (CPU test); returns the XCD block code
 int gemm_tile_order(int n_mt, int n_nt, int S, int BM, int BN, int K, int* mt, int* nt, int* z);
-constexpr int kGemmCfgs = 51;              // tile configurations (kernels_gemm.hip Cfg)
+constexpr int kGemmCfgs = 39;              // tile configurations (kernels_gemm.hip Cfg)
 
 // ---------------------------------------------------------------- decode GEMV
 struct StepState {  // device-resident decode step (read by kernels -> graph-replayable)

@@ -17,27 +17,26 @@ ARGS="--steps 16 --warmup 4 --no-cpu-baseline --no-api --prefill-iters 3 --kerne
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1
 echo trace done
-# SKIP_MFMA=1: keep the trace + HBM passes only (the every-leg MFMA pass can outlast its limit on a slow box)
+# FETCH_SIZE / WRITE_SIZE and the MFMA-busy pass over the short probe (prefill + eager decode, B = 1 and 8, and
+# the 448 px prefill): a TCC pass over bench.py's every-leg run does not finish, and (round 6) the SQ pass over
+# bench.py's graphed decode steps crashed the profiled process in hipGraph capture (host SIGSEGV in decode_step)
+P="python3 $R/tools/probes/pmc_probe.py 3 448"
+# SKIP_MFMA=1: keep the trace + HBM passes only
 if [ "${SKIP_MFMA:-0}" != 1 ]; then
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE \
-    --output-format csv -d $OUT/mfma -o run -- python3 $R/bench.py $ARGS > $OUT/mfma.log 2>&1
+    --output-format csv -d $OUT/mfma -o run -- $P > $OUT/mfma.log 2>&1
 echo mfma done
 fi
-# FETCH_SIZE / WRITE_SIZE over the short probe (prefill + eager decode, B = 1 and 8): a TCC pass
-# over bench.py's every-leg run does not finish
-P="python3 $R/tools/probes/pmc_probe.py 3"
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/ptrace -o run -- $P > $OUT/ptrace.log 2>&1
 echo probe trace done
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $P > $OUT/fetch.log 2>&1
 echo fetch done
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $P > $OUT/write.log 2>&1
 echo write done
-if [ "${SKIP_MFMA:-0}" != 1 ]; then
-python3 $R/tools/kernel_pmc.py $OUT/trace/run_kernel_trace.csv $OUT/mfma/run_counter_collection.csv \
-    - - $OUT/kernel_pmc_bench.csv > $OUT/summary.txt
-fi
-python3 $R/tools/kernel_pmc.py $OUT/ptrace/run_kernel_trace.csv - \
-    $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_hbm_probe.csv >> $OUT/summary.txt
+M=-
+[ "${SKIP_MFMA:-0}" != 1 ] && M=$OUT/mfma/run_counter_collection.csv
+python3 $R/tools/kernel_pmc.py $OUT/ptrace/run_kernel_trace.csv $M \
+    $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $OUT/kernel_hbm_probe.csv > $OUT/summary.txt
 echo done
 PGMI_ROUND=$TAG python3 $R/tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     "k_gemv<1, 4, 1, 2, 1, true, 1, false>" gateup $OUT/pmc_traffic.json >> $OUT/summary.txt

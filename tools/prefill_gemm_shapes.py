@@ -1,10 +1,8 @@
 """Per-shape durations of the prefill MLP GEMMs from a rocprofv3 kernel trace (run_kernel_trace.csv).
 
-One kernel template can serve several GEMM shapes (the M = 288 text o_proj and down projections are
-both W128x128 split 4 on the same grid), so a per-template average (kernel_stats.csv) mixes them.
-Each launch is labelled by its template and the kernel before it in the trace: a W128x128 split
-launch right after the GeGLU GEMM (or after another down launch: bench.py's back-to-back graph) is
-the down projection; others are o_proj.  Output: CSV label, template, launches, mean / median us --
+One kernel template can serve several GEMM shapes (until round 6 the M = 288 text o_proj and down
+projections were both W128x128 split 4 on the same grid), so a per-template average (kernel_stats.csv)
+may mix them; each launch is labelled by its template (and, for the 8-image down, the kernel before it).  Output: CSV label, template, launches, mean / median us --
 the figures bench.py's prefill_gemm_roofline (in situ, HIP events) is checked against.
 usage: python tools/prefill_gemm_shapes.py TRACE.csv OUT.csv
 """
@@ -12,12 +10,13 @@ import csv
 import statistics
 import sys
 
-GU224 = "k_gemm_w<8, 2, 9, 1, 2, 3, 4, 7, false>"   # W288n dual, GeGLU epilogue (M = 288)
-W128S = "k_gemm_w<8, 2, 4, 2, 1, 4, 4, 0, true>"    # W128x128 split (text o_proj / down at M = 288)
-GU448 = "k_gemm_8p<6, 7, false>"                    # E192, GeGLU (M = 1056)
-DN448 = "k_gemm_8p<6, 0, true>"                     # E192 split 4 (M = 1056 down)
-GU8 = "k_gemm_8p<8, 7, false>"                      # E256, GeGLU (M = 2304)
-DN8 = "k_gemm_w<8, 2, 9, 2, 1, 3, 4, 0, true>"       # W288w split 2 (M = 2304 down)
+GU224 = "k_gemm_w<8, 2, 9, 1, 2, 3, 4, 7, false, true>"   # R288w dual (in-wave reload), GeGLU epilogue (M = 288)
+DN224 = "k_gemm_w<8, 2, 9, 1, 1, 3, 4, 0, true, false>"   # W288n split 8 (text down at M = 288, round 6)
+W128S = "k_gemm_w<8, 2, 4, 2, 1, 4, 4, 0, true, false>"   # W128x128 split 4 (text o_proj at M = 288)
+GU448 = "k_gemm_8p<6, 7, false>"                          # E192, GeGLU (M = 1056)
+DN448 = "k_gemm_8p<6, 0, true>"                           # E192 split 5 (M = 1056 down)
+GU8 = "k_gemm_8p<8, 7, false>"                            # E256, GeGLU (M = 2304)
+DN8 = "k_gemm_w<8, 2, 9, 2, 1, 3, 4, 0, true, false>"     # W288w split 2 (M = 2304 down)
 
 
 def main(trace, out):
@@ -31,8 +30,10 @@ def main(trace, out):
         key = None
         if GU224 in name:
             key = ("224 gate|up + GeGLU (M=288)", GU224)
+        elif DN224 in name:
+            key = ("224 down (M=288)", DN224)
         elif W128S in name:
-            key = ("224 down (M=288)", W128S) if (GU224 in prev or W128S in prev) else ("224 o_proj (M=288)", W128S)
+            key = ("224 o_proj (M=288)", W128S)
         elif GU448 in name:
             key = ("448 gate|up + GeGLU (M=1056)", GU448)
         elif DN448 in name:

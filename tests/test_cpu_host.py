@@ -227,17 +227,19 @@ def test_ablation_patches_restated_match_reference_semantics():
 
 
 def test_prefill_gemm_shape_labels(tmp_path):
-    """tools/prefill_gemm_shapes.py splits one kernel template's launches by shape: a W128x128 split launch
-    after the GeGLU GEMM (or after another one: bench.py's back-to-back graph) is the down projection, any
-    other is o_proj -- the per-shape figures bench.py's in-situ prefill_gemm_roofline is checked against."""
+    """tools/prefill_gemm_shapes.py labels the prefill MLP GEMMs of a kernel trace by template (round 6: the
+    M = 288 down runs W288n split 8, its own template, and o_proj W128x128 split 4); a W288w split launch is
+    the 8-image down only right after the 8-image gate|up -- the per-shape figures bench.py's in-situ
+    prefill_gemm_roofline is checked against."""
     import csv
     import importlib.util
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     spec = importlib.util.spec_from_file_location("pgs", os.path.join(root, "tools", "prefill_gemm_shapes.py"))
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
-    seq = [("k_attn_fs", 5), (m.W128S, 10), ("k_splitk", 3), (m.GU224, 44), (m.W128S, 36), ("k_splitk", 3),
-           (m.GU224, 44), (m.W128S, 36), (m.W128S, 38), ("x", 1), (m.GU448, 126), (m.DN448, 72)]
+    seq = [("k_attn_fs", 5), (m.W128S, 10), ("k_splitk", 3), (m.GU224, 44), (m.DN224, 36), ("k_splitk", 3),
+           (m.GU224, 44), (m.DN224, 36), (m.DN224, 38), ("x", 1), (m.GU448, 126), (m.DN448, 72),
+           (m.DN8, 50), (m.GU8, 300), (m.DN8, 200)]
     tr = tmp_path / "trace.csv"
     with open(tr, "w", newline="") as f:
         w = csv.writer(f)
@@ -251,4 +253,5 @@ def test_prefill_gemm_shape_labels(tmp_path):
     rows = {r["label"]: r for r in csv.DictReader(open(out))}
     assert rows["224 o_proj (M=288)"]["launches"] == "1" and float(rows["224 o_proj (M=288)"]["mean_us"]) == 10
     assert rows["224 down (M=288)"]["launches"] == "3" and float(rows["224 down (M=288)"]["median_us"]) == 36
+    assert rows["8-image down (M=2304)"]["launches"] == "1" and float(rows["8-image down (M=2304)"]["mean_us"]) == 200
     assert float(rows["448 gate|up + GeGLU (M=1056)"]["mean_us"]) == 126

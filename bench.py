@@ -329,6 +329,33 @@ def time_sampling(eng, V, iters=20):
     return round(e0.elapsed_time(e1) * 1e3 / iters, 2)
 
 
+def decode_chunk(B, steps, warmup, graph=True):
+    """Greedy steps per hipGraph launch for a B-row decode run (Engine.generate's form): GEN_CHUNK
+    (pgmi_decode_steps) for the batched rows, where it measured faster (B = 8 step 1.279 -> 1.271 ms,
+    tools/probes/multistep_probe.py, profiles/r06_multistep_probe.txt); one step per launch at B <= 2, where it
+    measured slower (1.056 -> 1.060 ms).  Halved until it divides the timed steps and two chunks fit in the
+    warmup (the first call with a buffer set runs eagerly, the second captures the graph)."""
+    from pgmi import Engine
+    c = Engine.GEN_CHUNK if (graph and B >= Engine.GEN_MIN_BATCH) else 1
+    while c > 1 and (steps % c or warmup < 2 * c):
+        c //= 2
+    return c
+
+
+def run_decode(eng, cur, kv, L, step0, n, chunk, logits, graph):
+    """n greedy steps from KV row L + step0 (position one past it), the argmax fed back in place: chunks of
+    `chunk` steps per pgmi_decode_steps call (one graph launch), single pgmi_decode calls otherwise."""
+    t = 0
+    while t < n:
+        k = chunk if n - t >= chunk else 1
+        s0 = step0 + t
+        if k > 1:
+            eng.decode_steps(cur, kv, L + s0, L + s0 + 1, k, logits=logits, graph=graph)
+        else:
+            eng.decode(cur, kv, L + s0, L + s0 + 1, logits=logits, next_ids=cur, graph=graph)
+        t += k
+
+
 def time_batch(cfg, dev, seed, g, B, steps, warmup):
     """BASELINE configs[3], per GPU: B images (8 of the 64) through a B-row prefill, then
     lock-step KV-cached greedy decode of B sequences (graph replay, device argmax)."""
@@ -348,24 +375,17 @@ def time_batch(cfg, dev, seed, g, B, steps, warmup):
     pm, _, _, lg = time_prefill(e, px, ids, torch.arange(L).expand(B, L), kv, 5)
     cur = e.argmax(lg[:, 0])
     logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device=dev)
-    step = 0
-
-    def decode_step():
-        nonlocal step
-        step += 1
-        e.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=cur, graph=True)
-    for _ in range(warmup):
-        decode_step()
+    chunk = decode_chunk(B, steps, warmup)
+    run_decode(e, cur, kv, L, 0, warmup, chunk, logits, True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        decode_step()
+    run_decode(e, cur, kv, L, warmup, steps, chunk, logits, True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     del e
     torch.cuda.empty_cache()
     return {"images_per_gpu": B, "prefill_ms": round(pm, 3), "decode_tok_s": round(B * steps / dt, 1),
-            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps}
+            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "steps_per_graph_launch": chunk}
 
 
 def time_b1_full_length(eng, first, L, n_tokens=256):
@@ -694,22 +714,15 @@ def main():
     cur = first.clone()
     logits = torch.empty((B, cfg["text_config"]["vocab_size"]), dtype=torch.float32, device=dev)
     graph = not a.no_graph
-    step = 0
-
-    def decode_step():
-        nonlocal step
-        step += 1
-        # greedy feedback in place: the step reads cur's tokens first and writes the next ones last
-        eng.decode(cur, kv, L + step - 1, L + step, logits=logits, next_ids=cur, graph=graph)
-
-    for _ in range(a.warmup):
-        decode_step()
+    # greedy feedback in place (the step reads cur's tokens first and writes the next ones last); the
+    # batched rows (B >= 3: configs[3], the multi-GPU runs) launch several steps per graph (decode_chunk)
+    chunk = decode_chunk(B, a.steps, a.warmup, graph)
+    run_decode(eng, cur, kv, L, 0, a.warmup, chunk, logits, graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        decode_step()
+    run_decode(eng, cur, kv, L, a.warmup, a.steps, chunk, logits, graph)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -758,7 +771,7 @@ def main():
     batch8 = None
     if world == 1 and not a.no_extra and B == 1:
         # configs[3] at its stated length: 256 output tokens per image (SURVEY sec.8d cfg 4)
-        batch8 = time_batch(cfg, dev, a.seed, g, 8, 256, 8)
+        batch8 = time_batch(cfg, dev, a.seed, g, 8, 256, 16)
     api = None
     if world == 1 and not a.no_api and B == 1 and a.image_size == 224:
         api = time_api(cfg, dev, a.seed, a.api_tokens)
@@ -819,7 +832,7 @@ def main():
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": B * world, "prompt_len": L,
                        "images_gathered": int(gathered.shape[0]),
                        "decode_tokens_timed": a.steps, "parallelism": f"replicas x{world} (weights RCCL-broadcast)",
-                       "hipgraph": graph},
+                       "hipgraph": graph, "steps_per_graph_launch": chunk},
             "prefill_ms": round(prefill_ms, 3),
             "prefill_vision_ms": round(vision_ms, 3),
             "prefill_lm_ms": round(lm_ms, 3),

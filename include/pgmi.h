@@ -135,6 +135,14 @@ int pgmi_lm_forward(pgmi_ctx* ctx, const int64_t* ids, const void* image_feats, 
  *   argmax back in place (tokens are read first, the next ones written last): no staging copy. */
 int pgmi_decode(pgmi_ctx* ctx, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
                 int position, float* logits, int64_t* next_ids, int use_graph, void* stream);
+/* n_steps greedy decode steps back to back in one call (one hipGraph launch when use_graph != 0):
+ * the generate loop of inference.py:56-78 without sampling, as Engine.generate runs it.  ids (device
+ * int64 [B]) holds the input tokens and receives each step's argmax in place (step t + 1 reads step t's);
+ * the steps write KV rows kv_len .. kv_len + n_steps - 1 at positions position .. position + n_steps - 1;
+ * logits (device fp32 [B][vocab]) holds the last step's; tokens (device int64 [n_steps][B], may be
+ * NULL) records every step's argmax.  Each step is pgmi_decode's step, kernel for kernel. */
+int pgmi_decode_steps(pgmi_ctx* ctx, int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len,
+                      int position, int n_steps, float* logits, int64_t* tokens, int use_graph, void* stream);
 /* The same decode step with already-merged input rows instead of token ids: embeds (device bf16
  * [B][hidden]) is the output of a caller's _merge_input_ids_with_image_features for a q_len == 1
  * step (the ablation harness monkey-patches the merge, ablation_study_fixed.py:99-142,335-337,

@@ -63,9 +63,12 @@ struct GraphKey {
     const int64_t* ids;  // the ids buffer the graph reads (the context's staging copy, or in place)
     bool emb;            // the step's input is the staged embedding rows (pgmi_decode_embeds), not ids
     int masked;          // 0: no mask (a zero word), 1: staged bf16 mask (sum rounded), 2: staged fp32 mask
+    int n_steps;         // decode steps captured back to back (pgmi_decode_steps; 1 otherwise)
+    int64_t* tokens;     // their per-step token record ([n_steps][B], may be null)
     bool operator<(const GraphKey& o) const {
-        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids, emb, masked) <
-               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids, o.emb, o.masked);
+        return std::tie(B, kv, kv_batch, kv_max, logits, next, ids, emb, masked, n_steps, tokens) <
+               std::tie(o.B, o.kv, o.kv_batch, o.kv_max, o.logits, o.next, o.ids, o.emb, o.masked, o.n_steps,
+                        o.tokens);
     }
 };
 
@@ -951,7 +954,7 @@ static bool mf_staged(const pgmi_ctx* x) { return x->mf_staged > 0; }
 
 static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, void* kv, int kv_batch, int kv_max,
                        int launch_keys, float* logits, int64_t* next_ids, const uint16_t* embeds = nullptr,
-                       int masked = 0) {
+                       int masked = 0, int64_t* hist = nullptr) {
     const pgmi_config& c = x->c;
     const int H = c.t_hidden, NH = c.t_heads, NKV = c.t_kv_heads, HD = c.t_head_dim;
     const float eps = c.t_rms_eps;
@@ -1015,8 +1018,8 @@ static int decode_body(pgmi_ctx* x, hipStream_t s, const int64_t* ids, int B, vo
     // the step's last work also advances the device step state (pgmi_decode skips its host-side
     // set when the next call continues the sequence): lm_head's last workgroup, or argmax_finish
     if (!gemv_logits(s, B, x->dH, W(x, "language_model.model.norm.weight"), eps, E, c.t_vocab, logits, x->pmax,
-                     x->pidx, &nparts, x->lm_done, nx, x->step))
-        argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step);
+                     x->pidx, &nparts, x->lm_done, nx, x->step, hist))
+        argmax_finish(s, B, x->pmax, x->pidx, nparts, nx, x->step, hist);
     return 0;
 }
 
@@ -1111,12 +1114,14 @@ static int ensure_mf_image(pgmi_ctx* x, hipStream_t s) {
 
 static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int B, void* kv, int kv_batch, int kv_max,
                        int kv_len, int position, float* logits, int64_t* next_ids, int use_graph, void* stream,
-                       const DevStepIn* dev = nullptr) {
+                       const DevStepIn* dev = nullptr, int n_steps = 1, int64_t* tokens = nullptr) {
     int rc;
     if ((rc = ensure_prepared(x))) return rc;
     const pgmi_config& c = x->c;
     if (B < 1 || B > c.max_batch || B > kv_batch) return fail(PGMI_E_ARG, "batch exceeds capacity");
-    if (kv_len < 0 || kv_len >= kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
+    if (n_steps < 1) return fail(PGMI_E_ARG, "n_steps must be >= 1");
+    if (n_steps > 1 && (!ids || embeds || dev)) return fail(PGMI_E_ARG, "multi-step decode: token ids only");
+    if (kv_len < 0 || (long)kv_len + n_steps - 1 >= kv_max) return fail(PGMI_E_ARG, "KV cache capacity exceeded");
     if (kv_max > c.max_kv) return fail(PGMI_E_ARG, "kv_max exceeds config max_kv");
     if ((!ids && !embeds) || !kv || !logits) return fail(PGMI_E_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
@@ -1133,12 +1138,12 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         set_step(s, x->step, kv_len, position);
     }
     // the step advances the device state itself (its last kernel); known only once this call has
-    // enqueued its step successfully
+    // enqueued its steps successfully
     x->step_known = false;
     auto advanced = [&]() {
         x->step_known = dev == nullptr;
-        x->step_kv = kv_len + 1;
-        x->step_pos = position + 1;
+        x->step_kv = kv_len + n_steps;
+        x->step_pos = position + n_steps;
     };
     // input rows are always staged into the context's buffer (a stable address the graph reads)
     const uint16_t* erows = nullptr;
@@ -1146,9 +1151,19 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         HIPCHK(hipMemcpyAsync(x->d_emb, embeds, (size_t)B * c.t_hidden * 2, hipMemcpyDeviceToDevice, s));
         erows = x->d_emb;
     }
+    // n_steps greedy steps back to back: step t > 0 reads the argmax step t - 1 wrote (next_ids, or the
+    // context's d_next when the caller passes none); step t's token also goes to tokens[t][B] when given
+    int64_t* fb = next_ids ? next_ids : x->d_next;
+    auto body = [&](hipStream_t st, const int64_t* first, int keys0, bool grow) -> int {
+        for (int t = 0; t < n_steps; ++t) {
+            const int r = decode_body(x, st, t == 0 ? first : fb, B, kv, kv_batch, kv_max, grow ? keys0 + t : keys0,
+                                      logits, next_ids, erows, masked, tokens ? tokens + (long)t * B : nullptr);
+            if (r) return r;
+        }
+        return 0;
+    };
     if (!use_graph) {
-        if ((rc = decode_body(x, s, ids, B, kv, kv_batch, kv_max, kv_len + 1, logits, next_ids, erows, masked)))
-            return rc;
+        if ((rc = body(s, ids, kv_len + 1, true))) return rc;
         LAUNCHCHK();
         advanced();
         return 0;
@@ -1161,12 +1176,11 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         gids = x->d_ids;
     }
     if (embeds) gids = nullptr;
-    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids, embeds != nullptr, masked};
+    GraphKey key{B, kv, kv_batch, kv_max, logits, next_ids, gids, embeds != nullptr, masked, n_steps, tokens};
     GraphEntry& ge = x->graphs[key];
     if (!ge.exec) {
         if (ge.seen++ == 0) {  // first call with this key: run eagerly (sets kernel attributes)
-            if ((rc = decode_body(x, s, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked)))
-                return rc;
+            if ((rc = body(s, gids, kv_max, false))) return rc;
             LAUNCHCHK();
             advanced();
             return 0;
@@ -1174,7 +1188,7 @@ static int decode_step(pgmi_ctx* x, const int64_t* ids, const void* embeds, int 
         HIPCHK(hipStreamSynchronize(s));
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(x->cap_stream, hipStreamCaptureModeThreadLocal));
-        rc = decode_body(x, x->cap_stream, gids, B, kv, kv_batch, kv_max, kv_max, logits, next_ids, erows, masked);
+        rc = body(x->cap_stream, gids, kv_max, false);
         HIPCHK(hipStreamEndCapture(x->cap_stream, &g));
         if (rc) return rc;
         HIPCHK(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
@@ -1190,6 +1204,13 @@ int pgmi_decode(pgmi_ctx* x, const int64_t* ids, int B, void* kv, int kv_batch, 
                 float* logits, int64_t* next_ids, int use_graph, void* stream) {
     if (!ids) return fail(PGMI_E_ARG, "null argument");
     return decode_step(x, ids, nullptr, B, kv, kv_batch, kv_max, kv_len, position, logits, next_ids, use_graph, stream);
+}
+
+int pgmi_decode_steps(pgmi_ctx* x, int64_t* ids, int B, void* kv, int kv_batch, int kv_max, int kv_len, int position,
+                      int n_steps, float* logits, int64_t* tokens, int use_graph, void* stream) {
+    if (!ids) return fail(PGMI_E_ARG, "null argument");
+    return decode_step(x, ids, nullptr, B, kv, kv_batch, kv_max, kv_len, position, logits, ids, use_graph, stream,
+                       nullptr, n_steps, tokens);
 }
 
 int pgmi_decode_embeds(pgmi_ctx* x, const void* embeds, int B, void* kv, int kv_batch, int kv_max, int kv_len,

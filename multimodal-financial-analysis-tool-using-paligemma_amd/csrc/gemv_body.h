@@ -44,6 +44,7 @@ struct GemvArgs {
     unsigned* done;
     int64_t* next;
     StepState* adv;
+    int64_t* hist;  // (may be null) also receives next[b]: a multi-step graph's token record (pgmi_decode_steps)
     // QKV
     const uint16_t* cosT;
     const uint16_t* sinT;
@@ -556,6 +557,7 @@ __device__ __forceinline__ void gemv_block(const GemvArgs& a, const int blk, con
                         for (int q = 1; q < 4; ++q)
                             if (bv[q][0] > m || (bv[q][0] == m && bi[q][0] < mi)) { m = bv[q][0]; mi = bi[q][0]; }
                         a.next[b] = mi;
+                        if (a.hist) a.hist[b] = mi;
                     }
                 }
                 if (tid == 0) {

@@ -138,7 +138,7 @@ bool gemv_logits_folds(int B) { return B < gemv_mf_min_batch(); }
 
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps, const uint16_t* E,
                  int V, float* logits, float* pmax, int* pidx, int* nparts, unsigned* done, int64_t* next,
-                 StepState* adv) {
+                 StepState* adv, int64_t* hist) {
     GemvArgs a{};
     a.x = h; a.norm_w = norm_w; a.eps = eps; a.W = E; a.n_units = V; a.K = 2048; a.nb = B; a.logits = logits;
     a.pmax = pmax; a.pidx = pidx;
@@ -153,6 +153,7 @@ bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w
         a.done = done;
         a.next = next;
         a.adv = adv;
+        a.hist = hist;
     }
 #define LG_(b_, rpw)                                                    \
     do {                                                                \

@@ -498,7 +498,7 @@ void pad_rows(hipStream_t s, const uint16_t* src, int rows, int K, int Kpad, uin
 
 // ---------------------------------------------------------------- argmax (first max, torch semantics)
 __global__ void k_argmax_finish(const float* __restrict__ pmax, const int* __restrict__ pidx, int nparts,
-                                int64_t* __restrict__ out, StepState* adv) {
+                                int64_t* __restrict__ out, StepState* adv, int64_t* __restrict__ hist) {
     const int b = blockIdx.x;
     // the decode step's last kernel: every reader of the step state is done, so advance it to
     // the next step's (kv_len + 1, position + 1); pgmi_decode then skips its host-side set
@@ -529,12 +529,15 @@ __global__ void k_argmax_finish(const float* __restrict__ pmax, const int* __res
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[b] = si[0];
+    if (threadIdx.x == 0) {
+        out[b] = si[0];
+        if (hist) hist[b] = si[0];
+    }
 }
 
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
-                   StepState* adv) {
-    hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out, adv);
+                   StepState* adv, int64_t* hist) {
+    hipLaunchKernelGGL(k_argmax_finish, dim3(B), dim3(256), 0, s, pmax, pidx, nparts, out, adv, hist);
 }
 
 // ---------------------------------------------------------------- stop tokens of the batched loop
@@ -622,7 +625,7 @@ void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, in
     const int slice = ((V + nb - 1) / nb + 3) & ~3;
     nb = (V + slice - 1) / slice;
     hipLaunchKernelGGL(k_argmax_part, dim3(nb, rows), dim3(256), 0, s, x, V, slice, pmax, pidx, out);
-    if (nb > 1) hipLaunchKernelGGL(k_argmax_finish, dim3(rows), dim3(256), 0, s, pmax, pidx, nb, out, nullptr);
+    if (nb > 1) hipLaunchKernelGGL(k_argmax_finish, dim3(rows), dim3(256), 0, s, pmax, pidx, nb, out, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------- synthetic weights (bench / tests)

@@ -115,10 +115,12 @@ int gemv_mf_min_batch();  // smallest batch on the MFMA decode projections
 // advance the step state there; returns true when it did (no argmax_finish needed)
 bool gemv_logits(hipStream_t s, int B, const uint16_t* h, const uint16_t* norm_w, float eps,
                  const uint16_t* E, int V, float* logits, float* pmax, int* pidx, int* nparts,
-                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr);
-// adv (may be null): the decode step state, advanced by one step (the step's last kernel)
+                 unsigned* done = nullptr, int64_t* next = nullptr, StepState* adv = nullptr,
+                 int64_t* hist = nullptr);
+// adv (may be null): the decode step state, advanced by one step (the step's last kernel); hist (may be
+// null): a second destination of the argmax (a multi-step graph's per-step token record)
 void argmax_finish(hipStream_t s, int B, const float* pmax, const int* pidx, int nparts, int64_t* out,
-                   StepState* adv = nullptr);
+                   StepState* adv = nullptr, int64_t* hist = nullptr);
 int argmax_scratch_parts();
 void argmax_rows(hipStream_t s, const float* x, int rows, int V, float* pmax, int* pidx, int64_t* out);
 void eos_update(hipStream_t s, int64_t* next, int* finished, int B, int64_t eos, int64_t pad, int* n_alive);

@@ -65,6 +65,7 @@ SIGNATURES = {
     "pgmi_embed": (i32, [vp, vp, i32, vp, vp]),
     "pgmi_lm_forward": (i32, [vp, vp, vp, i32, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
     "pgmi_decode": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
+    "pgmi_decode_steps": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, i32, vp]),
     "pgmi_decode_embeds": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
     "pgmi_decode_embeds_dev": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, i32, vp, i32, i64, vp, vp, i32, vp]),
     "pgmi_set_prefill_graph": (i32, [vp, i32]),

@@ -44,6 +44,12 @@ def config_dict(cfg) -> dict:
 
 
 class Engine:
+    # generate(): greedy steps per hipGraph launch (pgmi_decode_steps) for batches of GEN_MIN_BATCH rows or more.
+    # Same box (tools/probes/multistep_probe.py): B = 8 step 1.279 -> 1.271 ms at 8-16 steps per launch, B = 1
+    # 1.056 -> 1.060 ms (slower: B <= 2 keeps one launch per step)
+    GEN_CHUNK = 8
+    GEN_MIN_BATCH = 3
+
     def __init__(self, cfg, device=None, max_batch: int = 8, max_seq: int = 1472, max_kv: Optional[int] = None):
         self.lib = N.lib()
         self.cfgd = config_dict(cfg)
@@ -301,6 +307,25 @@ class Engine:
                 "pgmi_decode")
         return logits
 
+    def decode_steps(self, ids: torch.Tensor, kv: torch.Tensor, kv_len: int, position: int, n_steps: int,
+                     logits: torch.Tensor = None, tokens: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
+        """n_steps greedy decode steps back to back (pgmi_decode_steps): ids (device int64, B) is read by the
+        first step and receives every step's argmax in place; tokens (int64 (n_steps, B), optional) records
+        them.  Returns the last step's logits (B, V) fp32."""
+        self._ready()
+        if ids.dtype is not torch.int64 or ids.device != self.device or not ids.is_contiguous():
+            raise ValueError("decode_steps: ids must be a contiguous int64 tensor on the engine's device (updated in place)")
+        B = ids.numel()
+        if logits is None:
+            logits = torch.empty((B, self.cfgd["t_vocab"]), dtype=torch.float32, device=self.device)
+        if tokens is not None and (tokens.dtype is not torch.int64 or tokens.device != self.device
+                                   or not tokens.is_contiguous() or tokens.numel() < n_steps * B):
+            raise ValueError("decode_steps: tokens must be a contiguous int64 (n_steps, B) tensor on the device")
+        N.check(self.lib.pgmi_decode_steps(self.ctx, ids.data_ptr(), B, kv.data_ptr(), kv.shape[2], kv.shape[3], kv_len,
+                                           position, int(n_steps), logits.data_ptr(), N.ptr(tokens), int(graph),
+                                           self._s()), "pgmi_decode_steps")
+        return logits
+
     def decode_embeds(self, embeds: torch.Tensor, kv: torch.Tensor, kv_len: int, position: int,
                       logits: torch.Tensor = None, graph: bool = False) -> torch.Tensor:
         """The decode step over already-merged input rows (B, hidden) bf16 -- a caller's merge for
@@ -425,6 +450,17 @@ class Engine:
             self._eos_update(cur, finished, int(eos_token_id), pad, alive)
             toks[:, 0] = cur
         n_done = n_tokens
+        if not do_sample and not stop and graph and n_tokens > 1 and B >= self.GEN_MIN_BATCH:
+            # greedy without a stop token: GEN_CHUNK steps per hipGraph launch (pgmi_decode_steps), the
+            # argmax fed back in place and every step's token kept in a device record
+            rec = torch.empty((self.GEN_CHUNK, B), dtype=torch.int64, device=self.device)
+            t = 1
+            while t < n_tokens:
+                n = min(self.GEN_CHUNK, n_tokens - t)
+                self.decode_steps(cur, kv, L + t - 1, L + t, n, logits=step_logits, tokens=rec, graph=graph)
+                toks[:, t:t + n] = rec[:n].t()
+                t += n
+            return (toks, torch.full((B,), n_tokens, dtype=torch.int64, device=self.device)) if return_lengths else toks
         for t in range(1, n_tokens):
             if stop and (t - 1) % max(1, sync_every) == 0 and int(alive.item()) == 0:
                 n_done = t

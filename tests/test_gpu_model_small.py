@@ -196,6 +196,53 @@ def test_batched_decode_matches_single(eng, gold):
         assert np.array_equal(tb[i], t1[0]), (i, tb[i], t1[0])
 
 
+@pytest.mark.parametrize("B", [1, 3])
+@pytest.mark.parametrize("graph", [False, True])
+def test_decode_steps_equal_single_steps(eng, gold, B, graph):
+    """pgmi_decode_steps (n greedy steps per call, one hipGraph launch at graph=True; Engine.generate's greedy
+    loop) runs pgmi_decode's step kernel for kernel: its token record, the ids fed back in place, the last
+    step's logits and the KV rows equal n single-step calls bit for bit -- on the eager first call, the
+    capturing second and a replay."""
+    px = torch.from_numpy(O.from_bits(gold["pixels_bits"])).cuda()
+    base = px[0]
+    pxs = torch.stack([base, base.flip(-1), base.flip(-2)][:B])
+    ids = torch.from_numpy(gold["ids"]).cuda().expand(B, -1).contiguous()
+    L = ids.shape[1]
+    n = 5
+    feats = eng.project(eng.vision(pxs))
+    V = eng.cfgd["t_vocab"]
+
+    def prefill(kv):
+        lg = eng.lm_forward(kv, 0, torch.arange(L).expand(B, L), ids=ids, image_feats=feats, logits_rows=1)[:, 0]
+        return eng.argmax(lg)
+
+    kv1 = eng.new_kv(B, L + n + 1)
+    first = prefill(kv1)
+    cur = first.clone()
+    lg1 = torch.empty((B, V), dtype=torch.float32, device="cuda")
+    ref = []
+    for t in range(n):
+        eng.decode(cur, kv1, L + t, L + t + 1, logits=lg1, next_ids=cur, graph=graph)
+        ref.append(cur.clone())
+    ref = torch.stack(ref)
+    kv2 = eng.new_kv(B, L + n + 1)
+    prefill(kv2)
+    cur2 = torch.empty_like(first)
+    rec = torch.empty((n, B), dtype=torch.int64, device="cuda")
+    lg2 = torch.empty((B, V), dtype=torch.float32, device="cuda")
+    for rep in range(3):
+        cur2.copy_(first)
+        rec.fill_(-1)
+        lg2.fill_(float("nan"))
+        eng.decode_steps(cur2, kv2, L, L + 1, n, logits=lg2, tokens=rec, graph=graph)
+        torch.cuda.synchronize()
+        assert torch.equal(rec, ref), (rep, rec, ref)
+        assert torch.equal(cur2, ref[-1]) and torch.equal(lg2, lg1), rep
+        assert torch.equal(kv2[:, :, :, :L + n], kv1[:, :, :, :L + n]), rep
+    with pytest.raises(ValueError):  # the n steps' KV rows must fit the cache
+        eng.decode_steps(cur2, kv2, L, L + 1, n + 2, logits=lg2, graph=graph)
+
+
 @pytest.mark.parametrize("B", [2, 8])
 def test_batched_decode_logits_match_single(eng, gold, B):
     """B lock-step sequences (BASELINE configs[3]: 8 images per GPU; B >= 3 runs the MFMA decode

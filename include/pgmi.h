@@ -268,6 +268,10 @@ int pgmi_sample_top_p(pgmi_ctx* ctx, const float* x, int rows, int V, float temp
  * 6 fp32 out (out is float*), 7 GeGLU with up rows at W + N*K */
 int pgmi_op_gemm(pgmi_ctx* ctx, const void* A, const void* W, int M, int N, int K, int epi, const void* bias,
                  const void* res, void* out, void* stream);
+/* pgmi_op_gemm with explicit row strides (elements, multiples of 8, >= K) of A and W: the prefill GEMMs'
+ * sensitivity to the operands' row pitch (tools/probes/stride_probe.py). */
+int pgmi_op_gemm_strided(pgmi_ctx* ctx, const void* A, int lda, const void* W, int ldw, int M, int N, int K, int epi,
+                         const void* bias, const void* res, void* out, void* stream);
 int pgmi_op_rmsnorm(pgmi_ctx* ctx, const void* x, const void* w, int rows, int D, float eps, void* out,
                     void* stream);
 int pgmi_op_layernorm(pgmi_ctx* ctx, const void* x, const void* w, const void* b, int rows, int D, float eps,

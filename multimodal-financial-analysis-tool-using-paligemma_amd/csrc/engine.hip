@@ -1481,6 +1481,25 @@ int pgmi_op_gemm(pgmi_ctx* x, const void* A, const void* Wt, int M, int N, int K
     return 0;
 }
 
+int pgmi_op_gemm_strided(pgmi_ctx* x, const void* A, int lda, const void* Wt, int ldw, int M, int N, int K, int epi,
+                         const void* bias, const void* res, void* out, void* stream) {
+    int rc;
+    if ((rc = ensure_prepared(x))) return rc;
+    if (K % 8 != 0 || lda < K || ldw < K || lda % 8 != 0 || ldw % 8 != 0)
+        return fail(PGMI_E_ARG, "K, lda, ldw must be multiples of 8 with lda, ldw >= K");
+    EpiArgs e{};
+    e.bias = reinterpret_cast<const uint16_t*>(bias);
+    e.res = reinterpret_cast<const uint16_t*>(res);
+    e.ldr = N;
+    e.ldo = N;
+    if (epi == EPI_F32) e.out_f32 = reinterpret_cast<float*>(out);
+    else e.out = reinterpret_cast<uint16_t*>(out);
+    gemm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(A), lda, reinterpret_cast<const uint16_t*>(Wt), ldw, M,
+         N, K, (Epi)epi, e, x->ws, x->ws_bytes, epi == EPI_GEGLU ? N : 0);
+    LAUNCHCHK();
+    return 0;
+}
+
 int pgmi_op_rmsnorm(pgmi_ctx* x, const void* in, const void* w, int rows, int D, float eps, void* out, void* stream) {
     if (!x) return fail(PGMI_E_ARG, "null ctx");
     rmsnorm((hipStream_t)stream, reinterpret_cast<const uint16_t*>(in), reinterpret_cast<const uint16_t*>(w), eps,

@@ -89,6 +89,7 @@ SIGNATURES = {
     "pgmi_tune_attention": (i32, [i32]),
     "pgmi_sample_top_p": (i32, [vp, vp, i32, i32, f32, f32, vp, vp, vp, vp]),
     "pgmi_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "pgmi_op_gemm_strided": (i32, [vp, vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "pgmi_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, f32, vp, vp]),
     "pgmi_op_layernorm": (i32, [vp, vp, vp, vp, i32, i32, f32, vp, vp]),
     "pgmi_op_attention": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp]),

@@ -9,7 +9,6 @@
 // P.V runs on MFMA from bf16 e = exp(s - m_c) (the reference rounds the normalised p to bf16,
 // modeling_gemma.py:273,277; here the unnormalised chunk-local e is rounded, the fp32 sum l_c
 // normalises at the combine: same rounding granularity, documented in DESIGN.md).
-#include "coh.h"
 #include "common.h"
 #include "launch.h"
 
@@ -31,10 +30,6 @@ __device__ __forceinline__ short8 frag256(const uint16_t* rowp, int kk, int lane
     return __builtin_bit_cast(short8, ldg16(rowp + k));
 }
 
-// COH (the batched attention + combine launch, kernels_fused.hip): the partial record is published
-// write-through and every lane's stores have drained when the block returns (after a barrier), so the
-// caller may count the chunk's arrival and another workgroup of the launch read the record coherently
-template <bool COH = false>
 __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepState* st, float* __restrict__ part,
                                                   int max_chunks, int chunk, int kvh, int b, unsigned char* lds) {
     const int kv_len = st->kv_len;
@@ -166,15 +161,11 @@ __device__ __forceinline__ void attn_decode_block(const AttnArgs& a, const StepS
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int h = (lane >> 4) * 4 + r;
-                if (h < a.G) stxf<COH>(pb + h * 256 + ct * 16 + li, acc[j][r]);
+                if (h < a.G) pb[h * 256 + ct * 16 + li] = acc[j][r];
             }
         }
     }
-    if (tid < 32) stxf<COH>(pb + 16 * 256 + tid, stat[tid >> 4][tid & 15]);
-    if constexpr (COH) {  // coh.h protocol: every lane drains its write-through stores before the count
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if (tid < 32) pb[16 * 256 + tid] = stat[tid >> 4][tid & 15];
 }
 
 }  // namespace pgmi

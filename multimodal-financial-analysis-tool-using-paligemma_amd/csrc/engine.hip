@@ -122,7 +122,6 @@ struct pgmi_ctx {
     float* d_zero;               // one zero word: the "no mask" mask of the decode attention
     int64_t* d_next;             // argmax target when the caller passes none
     unsigned* lm_done;           // lm_head arrival counter (argmax folded into its last workgroup)
-    unsigned* arrive_rows;       // per batch row: chunk counter of the batched attention + combine launch
     hipStream_t cap_stream = nullptr;
     std::map<GraphKey, GraphEntry> graphs;
     // prefill graphs (vision tower, language-model forward): replayed for repeated calls with
@@ -626,8 +625,6 @@ int pgmi_prepare(pgmi_ctx* x) {
         if ((rc = dalloc_t(x, &x->d_zero, 64))) return rc;
         HIPCHK(hipMemset(x->d_zero, 0, 64 * sizeof(float)));
         if ((rc = dalloc_t(x, &x->d_next, (size_t)B))) return rc;
-        if ((rc = dalloc_t(x, &x->arrive_rows, (size_t)B * 32))) return rc;
-        HIPCHK(hipMemset(x->arrive_rows, 0, (size_t)B * 32 * sizeof(unsigned)));
         if ((rc = dalloc_t(x, &x->lm_done, 33 * 32))) return rc;  // top word + 32 shards, a 128-B line each
         HIPCHK(hipMemset(x->lm_done, 0, 33 * 32 * sizeof(unsigned)));
         HIPCHK(hipStreamCreateWithFlags(&x->cap_stream, hipStreamNonBlocking));

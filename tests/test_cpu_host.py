@@ -255,3 +255,36 @@ def test_prefill_gemm_shape_labels(tmp_path):
     assert rows["224 down (M=288)"]["launches"] == "3" and float(rows["224 down (M=288)"]["median_us"]) == 36
     assert rows["8-image down (M=2304)"]["launches"] == "1" and float(rows["8-image down (M=2304)"]["mean_us"]) == 200
     assert float(rows["448 gate|up + GeGLU (M=1056)"]["mean_us"]) == 126
+
+
+def test_bench_decode_chunking():
+    """bench.py's batched decode legs (configs[3], the N > 1 lines) run the generate driver's steps per graph launch
+    (decode_chunk): GEN_CHUNK for 3+ rows, halved until it divides the timed steps and two chunks fit in the warmup
+    (the second call with a buffer set is the one that captures its graph); one step per launch for B <= 2 or
+    without graphs.  run_decode walks the KV rows and positions in order, chunk by chunk, singles at the tail."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    from pgmi import Engine
+    assert Engine.GEN_CHUNK == 8 and Engine.GEN_MIN_BATCH == 3
+    assert bench.decode_chunk(1, 20, 16) == 1 and bench.decode_chunk(2, 256, 16) == 1
+    assert bench.decode_chunk(8, 256, 16) == 8 and bench.decode_chunk(8, 20, 16) == 4
+    assert bench.decode_chunk(8, 20, 5) == 2 and bench.decode_chunk(8, 7, 16) == 1
+    assert bench.decode_chunk(8, 256, 16, graph=False) == 1 and bench.decode_chunk(3, 256, 0) == 1
+
+    class FakeEngine:
+        def __init__(self):
+            self.calls = []
+
+        def decode_steps(self, cur, kv, kv_len, position, n, logits=None, graph=False):
+            self.calls.append(("steps", kv_len, position, n))
+
+        def decode(self, cur, kv, kv_len, position, logits=None, next_ids=None, graph=False):
+            assert next_ids is cur  # greedy feedback in place
+            self.calls.append(("one", kv_len, position, 1))
+
+    e = FakeEngine()
+    bench.run_decode(e, "cur", None, 288, 0, 5, 2, None, True)
+    bench.run_decode(e, "cur", None, 288, 5, 8, 4, None, True)
+    assert e.calls == [("steps", 288, 289, 2), ("steps", 290, 291, 2), ("one", 292, 293, 1),
+                       ("steps", 293, 294, 4), ("steps", 297, 298, 4)]

@@ -105,6 +105,35 @@ def test_gemm_geglu(eng):
     assert rel_l2(got, ref) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,K,epi,pa,pw", [(288, 2560, 2048, 0, 64, 0), (256, 1152, 1152, 3, 8, 64),
+                                              (288, 512, 2048, 7, 64, 64), (288, 2048, 16384, 4, 0, 8)])
+def test_gemm_strided_matches_contiguous(eng, M, N, K, epi, pa, pw):
+    """pgmi_op_gemm_strided (the row-pitch probe's entry): A and W at row strides K + pa / K + pw give the
+    contiguous call's output bit for bit (same plan, same tiles, same order), and the pad columns are never
+    read (they hold NaN here)."""
+    from pgmi import _native as NN
+    rng = np.random.default_rng(M + N + K + epi)
+    rows_w = N * (2 if epi == 7 else 1)
+    A, Wt = bf(rand(rng, M, K)), bf(rand(rng, rows_w, K, scale=1 / np.sqrt(K)))
+    b, r = bf(rand(rng, N, scale=0.1)), bf(rand(rng, M, N))
+    Ap = torch.full((M, K + pa), float("nan"), dtype=torch.bfloat16, device="cuda")
+    Ap[:, :K] = A
+    Wp = torch.full((rows_w, K + pw), float("nan"), dtype=torch.bfloat16, device="cuda")
+    Wp[:, :K] = Wt
+    out0 = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+    out1 = torch.empty_like(out0)
+    s = NN.stream_handle()
+    NN.check(eng.lib.pgmi_op_gemm(eng.ctx, A.data_ptr(), Wt.data_ptr(), M, N, K, epi, b.data_ptr(), r.data_ptr(),
+                                  out0.data_ptr(), s))
+    NN.check(eng.lib.pgmi_op_gemm_strided(eng.ctx, Ap.data_ptr(), K + pa, Wp.data_ptr(), K + pw, M, N, K, epi,
+                                          b.data_ptr(), r.data_ptr(), out1.data_ptr(), s))
+    torch.cuda.synchronize()
+    assert torch.equal(out0, out1)
+    with pytest.raises(ValueError):  # a pitch below K
+        NN.check(eng.lib.pgmi_op_gemm_strided(eng.ctx, Ap.data_ptr(), K - 8, Wp.data_ptr(), K + pw, M, N, K, epi,
+                                              b.data_ptr(), r.data_ptr(), out1.data_ptr(), s))
+
+
 def test_rmsnorm(eng):
     from pgmi import _native as NN
     rng = np.random.default_rng(3)
